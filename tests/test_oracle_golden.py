@@ -1,0 +1,171 @@
+"""Pins the CPU oracle (oracle/lz4_oracle.c) to the reference's own outputs.
+
+Every fixture under tests/golden/ was produced by executing the reference
+JavaScript (tools/golden/gen_golden.mjs); the oracle must reproduce each one
+bit-for-bit. Runs on CPU only.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import cases_of, golden_bytes
+
+MESSAGES = {
+    -1: "LZ4: Output Buffer Too Small",
+    -2: "LZ4: Malformed Input",
+    -3: "LZ4: Invalid Offset 0",
+    -4: "LZ4: Dictionary Offset Out of Bounds",
+    -5: "LZ4: Invalid Magic Number",
+    -7: "LZ4: Content Checksum Error",
+}
+
+
+def _src_of(case):
+    if "gen" in case:
+        g = case["gen"]
+        return O.generate(g["gen"], g["seed"], g["n"])
+    return golden_bytes(case["src_file"]).copy()
+
+
+def test_xxh32_known_answers(manifest):
+    (c,) = cases_of(manifest, "xxh32")
+    base = O.generate(c["input"]["gen"], c["input"]["seed"], c["input"]["n"])
+    for n, h0, h1 in c["rows"]:
+        assert "%08x" % O.xxh32(base[:n], 0) == h0, n
+        assert "%08x" % O.xxh32(base[:n], 12345) == h1, n
+    for text, h in c["text"]:
+        assert "%08x" % O.xxh32(text.encode()) == h
+    assert O.xxh32(b"") == 0x02CC5D05 and O.xxh32(b"Hello World") == 0xB1FD16EE
+    assert "%08x" % O.xxh32(base[:1000]) == c["stateful_1000"]
+
+
+def test_block_compress_matches_reference(manifest):
+    cases = cases_of(manifest, "block")
+    assert len(cases) > 30
+    for c in cases:
+        src = _src_of(c)
+        assert "%08x" % O.xxh32(src) == c["src_xxh"], c["name"]      # generator parity with the JS one
+        comp = O.compress_block_bytes(src)
+        assert comp.size == c["comp_len"], c["name"]
+        assert "%08x" % O.xxh32(comp) == c["comp_xxh"], c["name"]
+        if c["comp_file"]:
+            assert np.array_equal(comp, golden_bytes(c["comp_file"])), c["name"]
+
+
+def test_block_decompress_spec_and_jscompat(manifest):
+    for c in cases_of(manifest, "block"):
+        src = _src_of(c)
+        comp = O.compress_block_bytes(src)
+        st, w, out = O.decompress_block(comp, src.size)
+        assert st == 0 and w == src.size and np.array_equal(out, src), c["name"]   # spec round trip
+        st, w, js = O.decompress_block(comp, src.size, js_compat=True)
+        assert st == 0 and w == c["js_dec_written"], c["name"]
+        if c["js_dec_equals_input"]:
+            assert np.array_equal(js, src), c["name"]
+        else:                                                                          # SURVEY F1 divergence
+            assert "%08x" % O.xxh32(js) == c["js_dec_xxh"], c["name"]
+            if c.get("js_dec_file"):
+                assert np.array_equal(js, golden_bytes(c["js_dec_file"])), c["name"]
+
+
+def test_block_chain_with_carried_table(manifest):
+    (c,) = cases_of(manifest, "block_chain")
+    g = c["gen"]
+    src = O.generate(g["gen"], g["seed"], g["n"])
+    out = np.zeros(400000, dtype=np.uint8)
+    table = np.full(16384, c["table_init"], dtype=np.int32)
+    pos = c["out_off0"]
+    for i, (start, n, expect) in enumerate(c["segments"]):
+        w, out, table = O.compress_block(src, start, n, table, out, pos)
+        assert w == expect
+        pos += w
+        if i == 0:
+            assert np.array_equal(table.view(np.uint8), golden_bytes(c["table1_file"]))
+    assert np.array_equal(out[:pos], golden_bytes(c["out_file"]))
+    assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_final_file"]))
+
+
+def test_decode_edge_cases(manifest):
+    (g,) = cases_of(manifest, "decode_cases")
+    for c in g["cases"]:
+        comp = np.array(c["comp"], dtype=np.uint8)
+        dic = None if c["dict"] is None else np.array(c["dict"], dtype=np.uint8)
+        out = np.zeros(c["out_len"], dtype=np.uint8)
+        st, w, out = O.decompress_block(comp, 0, out=out, out_off=c["out_off"], dictionary=dic, js_compat=True)
+        if c["ok"]:
+            assert st == 0, c["name"]
+            assert w == c["written"], c["name"]
+            assert out.tolist() == c["out"], c["name"]
+        else:
+            assert MESSAGES.get(st) == c["error"], (c["name"], st, c["error"])
+
+
+def test_frames_compress(manifest):
+    (g,) = cases_of(manifest, "frames")
+    inputs = {"text": ("text", 5, 300000), "copy": ("copy", 6, 150000), "tiles216": ("tiles216", 8, 1 << 20),
+              "random": ("random", 9, 70000)}
+    for f in g["frames"]:
+        name = f["input"]
+        if name in inputs:
+            data = O.generate(*inputs[name])[: f["n"]]
+        elif name == "hello":
+            data = b"Hello World"
+        elif name == "A10000":
+            data = b"A" * 10000
+        elif name == "empty":
+            data = b""
+        elif name == "dictmsg":
+            data = f["input_text"].encode()
+        dic = None
+        if "dict" in f:
+            d = f["dict"]
+            dic = O.generate(d["gen"], d["seed"], d["n"])
+        if "dict_text" in f:
+            dic = f["dict_text"].encode()
+        frame = O.compress_frame(data, dic, f["block"], f["indep"], f["checksum"], f.get("add_size", True))
+        assert frame.size == f["frame_len"], f
+        if "frame_hex" in f:
+            assert frame.tobytes().hex() == f["frame_hex"]
+        else:
+            assert "%08x" % O.xxh32(frame) == f["frame_xxh"], f
+        if f.get("frame_file"):
+            assert np.array_equal(frame, golden_bytes(f["frame_file"]))
+        verify = not f.get("noverify", False)
+        # js_compat decode reproduces the reference's decoder, including its
+        # F1 corruption and the resulting checksum failures
+        st, back = O.decompress_frame(frame, dic, verify_checksum=verify, js_compat=True)
+        if "dec_ok" in f:
+            if f["dec_ok"]:
+                assert st == 0, f
+                assert back.size == f["dec_len"] and "%08x" % O.xxh32(back) == f["dec_xxh"], f
+            else:
+                assert MESSAGES.get(st) == f["dec_error"], (st, f)
+        # the spec decoder always round-trips the reference's frames
+        st, back = O.decompress_frame(frame, dic)
+        assert st == 0 and back.tobytes() == bytes(np.frombuffer(bytes(data), dtype=np.uint8)), f
+
+
+def test_frames_decode_reference_vectors(manifest):
+    (g,) = cases_of(manifest, "frames")
+    for c in g["decode"]:
+        st, out = O.decompress_frame(bytes.fromhex(c["hex"]), verify_checksum=c["verify"], js_compat=True)
+        if c["ok"]:
+            assert st == 0, c["name"]
+            assert out.tobytes().hex() == c["out_hex"], c["name"]
+        elif st == -6:
+            assert c["error"].startswith("LZ4: Unsupported Version"), c["name"]
+        else:
+            assert MESSAGES.get(st) == c["error"], (c["name"], st)
+
+
+@pytest.mark.parametrize("kind", ["random", "repetitive", "tiles216"])
+def test_digest_manifest_4mib_subset(manifest, kind):
+    (g,) = cases_of(manifest, "digest_4mib")
+    rows = [r for r in g["rows"] if r["gen"] == kind][:3]          # full 16 seeds run on the GPU box
+    for r in rows:
+        src = O.generate(kind, r["seed"], r["n"])
+        assert "%08x" % O.xxh32(src) == r["src_xxh"]
+        comp = O.compress_block_bytes(src)
+        assert comp.size == r["comp_len"] and "%08x" % O.xxh32(comp) == r["comp_xxh"]
+        st, w, out = O.decompress_block(comp, src.size, js_compat=True)
+        assert st == 0 and w == r["js_dec_written"] and "%08x" % O.xxh32(out) == r["js_dec_xxh"]

@@ -1,0 +1,233 @@
+// tools/golden/gen_golden.mjs — generates tests/golden/ fixtures by EXECUTING the
+// reference JavaScript (mounted read-only at /root/reference) in the build
+// container. Run:  node tools/golden/gen_golden.mjs /root/reference tests/golden
+//
+// This script contains only our own input generators and harness code. It imports
+// the reference modules by absolute path at run time; nothing of the reference is
+// copied. Fixtures are data (inputs + the reference's outputs). The GPU box never
+// runs this script (the reference is not present there).
+import fs from 'fs';
+import path from 'path';
+
+const REF = process.argv[2] || '/root/reference';
+const OUT = process.argv[3] || 'tests/golden';
+// Node 12 has no top-level await: everything runs inside main().
+async function main() {
+const { compressBlock } = await import(path.join(REF, 'src/block/blockCompress.js'));
+const { decompressBlock } = await import(path.join(REF, 'src/block/blockDecompress.js'));
+const { xxHash32 } = await import(path.join(REF, 'src/xxhash32/xxhash32.js'));
+const { XXHash32 } = await import(path.join(REF, 'src/xxhash32/xxhash32Stateful.js'));
+const { compressBuffer } = await import(path.join(REF, 'src/buffer/bufferCompress.js'));
+const { decompressBuffer } = await import(path.join(REF, 'src/buffer/bufferDecompress.js'));
+
+fs.mkdirSync(path.join(OUT, 'bin'), { recursive: true });
+
+// ---- seeded generators (identical definitions to oracle/lz4_oracle.c orc_generate) ----
+function rng(seed) { let x = (seed >>> 0) || 1; return () => { x ^= x << 13; x >>>= 0; x ^= x >>> 17; x ^= x << 5; x >>>= 0; return x; }; }
+function gen(kind, seed, n) {
+    const r = rng(seed), b = new Uint8Array(n); let i = 0;
+    switch (kind) {
+        case 'random': for (i = 0; i < n; i += 4) { const v = r(); for (let k = 0; k < 4 && i + k < n; k++) b[i + k] = (v >>> (8 * k)) & 255; } break;
+        case 'repetitive': for (i = 0; i < n; i++) b[i] = i % 251; break;
+        case 'tiles216': {
+            const t = new Uint8Array(216 * 64); for (let k = 0; k < t.length; k++) t[k] = r() & 255;
+            while (i < n) { const base = 64 * (r() % 216); for (let k = 0; k < 64 && i < n; k++) b[i++] = t[base + k]; }
+            break;
+        }
+        case 'copy':
+            while (i < n) {
+                const L = 4 + r() % 5; for (let k = 0; k < L && i < n; k++) b[i++] = r() & 255;
+                const M = 48 + r() % 33, off = 16 + r() % 4081; if (i - off < 0) continue;
+                for (let k = 0; k < M && i < n; k++, i++) b[i] = b[i - off];
+            }
+            break;
+        case 'runs':
+            while (i < n) { const v = r() & 255, L = 1 + r() % 24; for (let k = 0; k < L && i < n; k++) b[i++] = v; }
+            break;
+        case 'text': {
+            const words = 'the of and to in is was for on that with as by at from his an were are which this be or has had not but it its'.split(' ');
+            while (i < n) {
+                const v = r(); const w = words[v % words.length];
+                for (let k = 0; k < w.length && i < n; k++) b[i++] = w.charCodeAt(k);
+                if (i < n) b[i++] = ((v >>> 16) % 11 === 0) ? 10 : 32;
+            }
+            break;
+        }
+        default: throw new Error('bad kind ' + kind);
+    }
+    return b;
+}
+
+const manifest = { generator: 'tools/golden/gen_golden.mjs', reference: 'divortio-lz4 @ /root/reference (executed under node ' + process.version + ')', cases: [] };
+let fileId = 0;
+function save(buf, tag) {
+    const name = `${String(fileId++).padStart(3, '0')}_${tag}.bin`;
+    fs.writeFileSync(path.join(OUT, 'bin', name), Buffer.from(buf.buffer, buf.byteOffset, buf.byteLength));
+    return 'bin/' + name;
+}
+// Large outputs are pinned by (length, xxh32) only; bytes are kept for small ones.
+const SMALL = 70000;
+function saveSmall(buf, tag) { return buf.length <= SMALL ? save(buf, tag) : null; }
+const hex = (u) => (u >>> 0).toString(16).padStart(8, '0');
+function tryCall(fn) { try { return { ok: true, value: fn() }; } catch (e) { return { ok: false, error: String(e.message) }; } }
+
+// ---- 1. xxHash32 known answers ------------------------------------------------
+{
+    const base = gen('random', 7, 1 << 20);
+    const rows = [];
+    for (let n = 0; n <= 64; n++) rows.push([n, hex(xxHash32(base.subarray(0, n), 0)), hex(xxHash32(base.subarray(0, n), 12345))]);
+    for (const n of [100, 1000, 4093, 65536, 1 << 20]) rows.push([n, hex(xxHash32(base.subarray(0, n), 0)), hex(xxHash32(base.subarray(0, n), 12345))]);
+    const st = new XXHash32(0); for (let p = 0; p < 1000; p += 37) st.update(base.subarray(p, Math.min(1000, p + 37)));
+    manifest.cases.push({ kind: 'xxh32', input: { gen: 'random', seed: 7, n: 1 << 20 }, rows,
+        text: [['', hex(xxHash32(new Uint8Array(0)))], ['Hello World', hex(xxHash32(new TextEncoder().encode('Hello World')))]],
+        stateful_1000: hex(st.digest()) });
+}
+
+// ---- 2. compressBlock / decompressBlock on fresh tables -----------------------
+const blockInputs = [];
+for (let n = 0; n <= 16; n++) blockInputs.push([`zeros${n}`, new Uint8Array(n)]);
+blockInputs.push(['zeros64', new Uint8Array(64)]);
+blockInputs.push(['A10000', new TextEncoder().encode('A'.repeat(10000))]);
+blockInputs.push(['hello', new TextEncoder().encode('Hello World')]);
+blockInputs.push(['utf8', new TextEncoder().encode('Hello \u{1F30D} World! ' + 'Repeat'.repeat(50))]);
+for (const n of [13, 100, 1000, 4096]) blockInputs.push([`random${n}`, gen('random', 3, n)]);
+for (const kind of ['random', 'repetitive', 'tiles216', 'copy', 'runs', 'text'])
+    for (const n of [65536, 262144]) blockInputs.push([`${kind}${n}`, gen(kind, 11, n), { gen: kind, seed: 11, n }]);
+blockInputs.push(['ramp60k', (() => { const b = new Uint8Array(60000); for (let i = 0; i < b.length; i++) b[i] = (i * 7 + (i >> 9)) & 255; return b; })()]);
+
+for (const [name, src, genSpec] of blockInputs) {
+    const out = new Uint8Array(src.length + (src.length / 255 | 0) + 16);
+    const table = new Int32Array(16384);
+    const n = compressBlock(src, out, 0, src.length, table, 0);
+    const comp = out.subarray(0, n);
+    const dec = new Uint8Array(src.length);
+    const d = tryCall(() => decompressBlock(comp, 0, comp.length, dec, 0));
+    let same = d.ok && dec.every((v, i) => v === src[i]);
+    const c = { kind: 'block', name, n: src.length, comp_len: n, comp_xxh: hex(xxHash32(comp)), src_xxh: hex(xxHash32(src)),
+        comp_file: saveSmall(comp, name + '_comp'), js_dec_ok: d.ok, js_dec_written: d.ok ? d.value : null, js_dec_equals_input: same };
+    if (genSpec) c.gen = genSpec; else c.src_file = save(src, name + '_src');  // non-generated inputs always kept
+    if (!same) { c.js_dec_file = saveSmall(dec, name + '_jsdec'); c.js_dec_xxh = hex(xxHash32(dec)); }
+    manifest.cases.push(c);
+}
+
+// ---- 3. compressBlock with a carried table, srcStart > 0, outputOffset > 0 -----
+{
+    const src = gen('copy', 21, 200000);
+    const out = new Uint8Array(400000);
+    const table = new Int32Array(16384).fill(-1);   // raw.test.mjs style (-1 == empty)
+    const n1 = compressBlock(src, out, 0, 65536, table, 7);
+    const t1 = new Int32Array(table);
+    const n2 = compressBlock(src, out, 65536, 100000, table, 7 + n1);
+    const n3 = compressBlock(src, out, 165536, 34464, table, 7 + n1 + n2);
+    manifest.cases.push({ kind: 'block_chain', gen: { gen: 'copy', seed: 21, n: 200000 }, table_init: -1, out_off0: 7,
+        segments: [[0, 65536, n1], [65536, 100000, n2], [165536, 34464, n3]],
+        out_file: save(out.subarray(0, 7 + n1 + n2 + n3), 'chain_out'), table1_file: save(t1, 'chain_table1'),
+        table_final_file: save(table, 'chain_table_final') });
+}
+
+// ---- 4. decompressBlock: errors, dictionaries, offsets ------------------------
+{
+    const cases = [];
+    const mk = (name, bytes, outLen, outOff = 0, dict = null) => {
+        const comp = Uint8Array.from(bytes);
+        const out = new Uint8Array(outLen);
+        const r = tryCall(() => decompressBlock(comp, 0, comp.length, out, outOff, dict));
+        cases.push({ name, comp: Array.from(comp), out_len: outLen, out_off: outOff, dict: dict ? Array.from(dict) : null,
+            ok: r.ok, written: r.ok ? r.value : null, error: r.ok ? null : r.error, out: r.ok ? Array.from(out) : null });
+    };
+    mk('lit_only', [0x50, 1, 2, 3, 4, 5], 5);
+    mk('too_small', [0x50, 1, 2, 3, 4, 5], 4);
+    mk('malformed_lit', [0x50, 1, 2, 3], 16);
+    mk('offset0', [0x10, 9, 0, 0], 16);
+    mk('dict_oob_nodict', [0x10, 9, 2, 0], 16);
+    mk('match_rle', [0x14, 7, 1, 0, 0x50, 1, 2, 3, 4, 5], 32);
+    mk('match_overlap4', [0x40, 1, 2, 3, 4, 4, 0, 0x50, 9, 9, 9, 9, 9], 32);
+    mk('match_long_varint', [0x1F, 42, 1, 0, 255, 3, 0x00], 400);
+    mk('match_overflow_drop', [0x1F, 42, 1, 0, 40], 30);
+    mk('dict_match', [0x0F, 8, 0, 5, 0x30, 7, 7, 7], 64, 0, Uint8Array.from([10, 11, 12, 13, 14, 15, 16, 17, 18, 19]));
+    mk('dict_match_spill', [0x05, 3, 0, 0x10, 1], 64, 0, Uint8Array.from([21, 22, 23, 24, 25]));
+    mk('dict_oob', [0x05, 30, 0], 64, 0, Uint8Array.from([1, 2, 3]));
+    mk('out_offset_history', [0x04, 3, 0, 0x10, 99], 32, 5);
+    mk('f1_trigger', [0x80, 1, 2, 3, 4, 5, 6, 7, 8, 0x01, 8, 0, 0x10, 77], 32);
+    mk('truncated_offset', [0x10, 5, 9], 16);
+    mk('empty', [], 16);
+    mk('token_only_zero', [0x00], 16);
+    manifest.cases.push({ kind: 'decode_cases', cases });
+}
+
+// ---- 5. frames ----------------------------------------------------------------
+{
+    const frames = [];
+    const inputs = [['text', gen('text', 5, 300000)], ['copy', gen('copy', 6, 150000)], ['tiles216', gen('tiles216', 8, 1 << 20)],
+        ['random', gen('random', 9, 70000)], ['hello', new TextEncoder().encode('Hello World')], ['empty', new Uint8Array(0)],
+        ['A10000', new TextEncoder().encode('A'.repeat(10000))]];
+    for (const [iname, input] of inputs) for (const bsz of [65536, 262144, 1048576, 4194304]) for (const indep of [true, false]) for (const cs of [false, true]) {
+        if (input.length > 300000 && bsz < 1048576 && !(indep && !cs)) continue;
+        const f = compressBuffer(input, null, bsz, indep, cs);
+        const back = tryCall(() => decompressBuffer(f));
+        frames.push({ input: iname, n: input.length, block: bsz, indep, checksum: cs, frame_len: f.length, frame_xxh: hex(xxHash32(f)),
+            frame_file: saveSmall(f, `frame_${iname}_${bsz}_${indep ? 'i' : 'd'}${cs ? 'c' : ''}`), dec_ok: back.ok, dec_error: back.ok ? null : back.error,
+            dec_xxh: back.ok ? hex(xxHash32(back.value)) : null, dec_len: back.ok ? back.value.length : null,
+            dec_equals_input: back.ok && back.value.length === input.length && back.value.every((v, i) => v === input[i]) });
+    }
+    // no content size, dictionary, outputBuffer path
+    const text = gen('text', 5, 300000);
+    const f1 = compressBuffer(text, null, 65536, false, true, false);
+    const b1 = tryCall(() => decompressBuffer(f1, null, false));
+    frames.push({ input: 'text', n: text.length, block: 65536, indep: false, checksum: true, add_size: false, frame_len: f1.length,
+        frame_xxh: hex(xxHash32(f1)), frame_file: saveSmall(f1, 'frame_text_nosize'), noverify: true, dec_ok: b1.ok, dec_error: b1.ok ? null : b1.error,
+        dec_xxh: b1.ok ? hex(xxHash32(b1.value)) : null, dec_len: b1.ok ? b1.value.length : null });
+    const dict = gen('text', 77, 70000);
+    for (const indep of [false, true]) {
+        const f2 = compressBuffer(text.subarray(0, 100000), dict, 65536, indep, true);
+        const back = tryCall(() => decompressBuffer(f2, dict));
+        frames.push({ input: 'text', n: 100000, block: 65536, indep, checksum: true, dict: { gen: 'text', seed: 77, n: 70000 }, frame_len: f2.length,
+            frame_xxh: hex(xxHash32(f2)), frame_file: saveSmall(f2, `frame_text_dict_${indep ? 'i' : 'd'}`), dec_ok: back.ok, dec_error: back.ok ? null : back.error,
+            dec_xxh: back.ok ? hex(xxHash32(back.value)) : null, dec_len: back.ok ? back.value.length : null,
+            dec_equals_input: back.ok && back.value.every((v, i) => v === text[i]) });
+    }
+    const small = new TextEncoder().encode('CommonPrefix_SharedData_Reference_1234567890_UniquePartA');
+    const sdict = new TextEncoder().encode('CommonPrefix_SharedData_Reference_1234567890');
+    const f3 = compressBuffer(small, sdict);
+    frames.push({ input: 'dictmsg', n: small.length, block: 4194304, indep: false, checksum: false, dict_text: 'CommonPrefix_SharedData_Reference_1234567890',
+        frame_len: f3.length, frame_hex: Buffer.from(f3).toString('hex'), input_text: 'CommonPrefix_SharedData_Reference_1234567890_UniquePartA' });
+    // decode-only frames (reference tests/golden.test.mjs vectors + corruptions)
+    const dec = [];
+    const dcase = (name, hexs, verify = true) => {
+        const b = Uint8Array.from(Buffer.from(hexs, 'hex'));
+        const r = tryCall(() => decompressBuffer(b, null, verify));
+        dec.push({ name, hex: hexs, verify, ok: r.ok, error: r.ok ? null : r.error, out_hex: r.ok ? Buffer.from(r.value).toString('hex') : null });
+    };
+    dcase('hello_spec', '04224D186040820B00008048656c6c6f20576f726c6400000000');
+    dcase('empty_4mb', '04224D1860707300000000');
+    dcase('hello_checksum', '04224D186440A70B00008048656c6c6f20576f726c6400000000EE16FDB1');
+    dcase('hello_badsum', '04224D186440A70B00008048656c6c6f20576f726c6400000000EE16FDB2');
+    dcase('hello_badsum_noverify', '04224D186440A70B00008048656c6c6f20576f726c6400000000EE16FDB2', false);
+    dcase('bad_magic', '000102030405');
+    dcase('bad_version', '04224D18A040820000000000');
+    const hw = compressBuffer(new TextEncoder().encode('Integrity Check'), null, 65536, false, true);
+    dcase('hw_roundtrip', Buffer.from(hw).toString('hex'));
+    manifest.cases.push({ kind: 'frames', frames, decode: dec });
+}
+
+// ---- 6. 4 MiB block digest manifest (full-size parity, GPU box regenerates) ----
+{
+    const rows = [];
+    const N = 4194304;
+    const out = new Uint8Array(N + (N / 255 | 0) + 16);
+    const dec = new Uint8Array(N);
+    for (const kind of ['random', 'repetitive', 'tiles216']) for (let seed = 1; seed <= 16; seed++) {
+        const src = gen(kind, seed, N);
+        const table = new Int32Array(16384);
+        const n = compressBlock(src, out, 0, N, table, 0);
+        const w = decompressBlock(out, 0, n, dec, 0);
+        rows.push({ gen: kind, seed, n: N, src_xxh: hex(xxHash32(src)), comp_len: n, comp_xxh: hex(xxHash32(out.subarray(0, n))),
+            js_dec_written: w, js_dec_xxh: hex(xxHash32(dec)) });
+    }
+    manifest.cases.push({ kind: 'digest_4mib', rows });
+}
+
+fs.writeFileSync(path.join(OUT, 'manifest.json'), JSON.stringify(manifest, null, 1));
+console.log('wrote', manifest.cases.length, 'case groups to', OUT);
+}
+main().catch((e) => { console.error(e); process.exit(1); });
