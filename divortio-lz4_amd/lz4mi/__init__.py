@@ -1,0 +1,245 @@
+"""Python binding of liblz4mi.so (include/lz4mi.h) — the MI355X LZ4 block codec.
+
+Used by bench.py, __graft_entry__ and the tests. Every compute entry point goes
+through the HIP C-ABI; there is no CPU fallback: if the library or a gfx950
+device is missing, calls raise Lz4miError.
+
+Mirrors the reference's raw-block and frame functions
+(src/block/blockCompress.js:31, src/block/blockDecompress.js:30,
+src/xxhash32/xxhash32.js:21) with the same argument meaning and error strings.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "liblz4mi.so")
+
+OK = 0
+ERR_OUTPUT_TOO_SMALL, ERR_MALFORMED, ERR_OFFSET0, ERR_DICT_OOB = -1, -2, -3, -4
+ERR_MAGIC, ERR_VERSION, ERR_CHECKSUM, ERR_RANGE, ERR_CROSS_BLOCK = -5, -6, -7, -8, -9
+ERR_HIP, ERR_ARG, ERR_NO_DEVICE = -100, -101, -102
+
+DEVICE_PTRS = 0x1
+JS_COMPAT = 0x2
+XXH_STANDARD = 0x4
+
+GEN_RANDOM, GEN_REPETITIVE, GEN_TILES216 = 0, 1, 2
+GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GEN_TILES216}
+
+# every symbol include/lz4mi.h declares (checked by tests/test_capi_cpu.py)
+EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_version",
+           "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
+           "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_generate_blocks")
+
+
+class Lz4miError(RuntimeError):
+    def __init__(self, status, message=None):
+        self.status = status
+        super().__init__(message or status_message(status))
+
+
+_lib = None
+_vp = ctypes.c_void_p
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise Lz4miError(ERR_NO_DEVICE, "liblz4mi.so not built (run __graft_entry__.build())")
+        # PyTorch wheels bundle their own libamdhip64 under a different file name;
+        # load torch first so one HIP runtime serves both (a second runtime
+        # instance in the process cannot see the GPU).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        L.lz4mi_status_message.restype = ctypes.c_char_p
+        L.lz4mi_status_message.argtypes = [ctypes.c_int32]
+        L.lz4mi_version.restype = ctypes.c_char_p
+        L.lz4mi_init.restype = ctypes.c_int32
+        L.lz4mi_init.argtypes = [ctypes.c_int32]
+        L.lz4mi_device_count.restype = ctypes.c_int32
+        L.lz4mi_decompress_blocks.restype = ctypes.c_int32
+        L.lz4mi_decompress_blocks.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
+                                              ctypes.c_uint32, ctypes.c_uint32, _vp]
+        L.lz4mi_compress_blocks.restype = ctypes.c_int32
+        L.lz4mi_compress_blocks.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
+        L.lz4mi_compress_block_table.restype = ctypes.c_int64
+        L.lz4mi_compress_block_table.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
+                                                 ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, _vp]
+        L.lz4mi_xxh32.restype = ctypes.c_uint32
+        L.lz4mi_xxh32.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32]
+        L.lz4mi_xxh32_blocks.restype = ctypes.c_int32
+        L.lz4mi_xxh32_blocks.argtypes = [_vp, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
+        L.lz4mi_generate_blocks.restype = ctypes.c_int32
+        L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, _vp]
+        _lib = L
+    return _lib
+
+
+def status_message(status):
+    return lib().lz4mi_status_message(int(status)).decode()
+
+
+def _check(st):
+    if st != OK:
+        raise Lz4miError(st)
+
+
+def init(device=-1):
+    _check(lib().lz4mi_init(device))
+
+
+def device_count():
+    return lib().lz4mi_device_count()
+
+
+def _p(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def _u8(x):
+    if x is None:
+        return None
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(x), dtype=np.uint8)
+    return np.ascontiguousarray(x, dtype=np.uint8)
+
+
+def compress_bound(n):
+    return n + n // 255 + 16
+
+
+# ---------------------------------------------------------------- host API
+def xxh32(data, seed=0, standard=False):
+    """xxHash32 (reference variant by default; host CPU, one serial chain)."""
+    a = _u8(data)
+    return lib().lz4mi_xxh32(_p(a), a.size, seed & 0xFFFFFFFF, XXH_STANDARD if standard else 0)
+
+
+def compress_blocks(blocks):
+    """Independent raw blocks -> list of compressed byte arrays (GPU)."""
+    arrs = [_u8(b) for b in blocks]
+    n = len(arrs)
+    if n == 0:
+        return []
+    in_len = np.array([a.size for a in arrs], dtype=np.uint32)
+    in_off = np.zeros(n, dtype=np.uint64)
+    in_off[1:] = np.cumsum(in_len[:-1].astype(np.uint64))
+    src = np.concatenate(arrs) if in_len.sum() else np.zeros(1, dtype=np.uint8)
+    bounds = np.array([compress_bound(int(x)) for x in in_len], dtype=np.uint64)
+    out_off = np.zeros(n, dtype=np.uint64)
+    out_off[1:] = np.cumsum(bounds[:-1])
+    out = np.zeros(int(bounds.sum()), dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint32)
+    _check(lib().lz4mi_compress_blocks(_p(src), _p(in_off), _p(in_len), _p(out), _p(out_off), _p(out_len), n, 0,
+                                       None))
+    return [out[int(o):int(o) + int(l)].copy() for o, l in zip(out_off, out_len)]
+
+
+def compress_block(data):
+    return compress_blocks([data])[0]
+
+
+def compress_raw(src, output, src_start, src_len, hash_table, output_offset):
+    """compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset) with
+    the reference's full semantics (table in/out, absolute positions)."""
+    s = _u8(src)
+    assert hash_table.dtype == np.int32 and hash_table.size == 16384 and hash_table.flags.c_contiguous
+    assert output.dtype == np.uint8 and output.flags.c_contiguous
+    r = lib().lz4mi_compress_block_table(_p(s), s.size, src_start, src_len, hash_table.ctypes.data,
+                                         _p(output), output.size, output_offset, 0, None)
+    if r < 0:
+        raise Lz4miError(int(r))
+    return int(r)
+
+
+def decompress_blocks(blocks, out_sizes, js_compat=False, dictionary=None):
+    """Independent compressed blocks -> (statuses, outputs) (GPU)."""
+    arrs = [_u8(b) for b in blocks]
+    n = len(arrs)
+    in_len = np.array([a.size for a in arrs], dtype=np.uint32)
+    in_off = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        in_off[1:] = np.cumsum(in_len[:-1].astype(np.uint64))
+    src = np.concatenate(arrs) if n and in_len.sum() else np.zeros(1, dtype=np.uint8)
+    out_cap = np.array(out_sizes, dtype=np.uint32)
+    out_off = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        out_off[1:] = np.cumsum(out_cap[:-1].astype(np.uint64))
+    out = np.zeros(max(1, int(out_cap.sum())), dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint32)
+    status = np.zeros(n, dtype=np.int32)
+    d = _u8(dictionary)
+    _check(lib().lz4mi_decompress_blocks(_p(src), _p(in_off), _p(in_len), _p(out), _p(out_off), _p(out_cap),
+                                         _p(d), 0 if d is None else d.size, _p(out_len), _p(status), n,
+                                         JS_COMPAT if js_compat else 0, None))
+    outs = [out[int(o):int(o) + min(int(l), int(c))].copy() for o, l, c in zip(out_off, out_len, out_cap)]
+    return status, outs, out_len
+
+
+def decompress_raw(inp, input_offset, input_size, output, output_offset=0, dictionary=None, js_compat=False):
+    """decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary):
+    writes into `output` (numpy uint8) and returns bytes written; raises with the
+    reference's message on error."""
+    a = _u8(inp)
+    seg = a[input_offset:input_offset + input_size]
+    in_off = np.zeros(1, dtype=np.uint64)
+    in_len = np.array([seg.size], dtype=np.uint32)
+    out_off = np.array([output_offset], dtype=np.uint64)
+    out_cap = np.array([max(0, output.size - output_offset)], dtype=np.uint32)
+    out_len = np.zeros(1, dtype=np.uint32)
+    status = np.zeros(1, dtype=np.int32)
+    d = _u8(dictionary)
+    seg = np.ascontiguousarray(seg) if seg.size else np.zeros(1, dtype=np.uint8)
+    _check(lib().lz4mi_decompress_blocks(_p(seg), _p(in_off), _p(in_len), _p(output), _p(out_off), _p(out_cap),
+                                         _p(d), 0 if d is None else d.size, _p(out_len), _p(status), 1,
+                                         JS_COMPAT if js_compat else 0, None))
+    if status[0] != OK:
+        raise Lz4miError(int(status[0]))
+    return int(out_len[0])
+
+
+def xxh32_blocks(blocks, seed=0, standard=False):
+    arrs = [_u8(b) for b in blocks]
+    n = len(arrs)
+    ln = np.array([a.size for a in arrs], dtype=np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    src = np.concatenate(arrs) if n and ln.sum() else np.zeros(1, dtype=np.uint8)
+    h = np.zeros(n, dtype=np.uint32)
+    _check(lib().lz4mi_xxh32_blocks(_p(src), _p(off), _p(ln), seed & 0xFFFFFFFF, _p(h), n,
+                                    XXH_STANDARD if standard else 0, None))
+    return h
+
+
+# -------------------------------------------------------------- device API
+# Raw device pointers (ints, e.g. torch tensor .data_ptr()) and a hipStream_t
+# handle (int, e.g. torch.cuda.current_stream().cuda_stream). Async.
+def decompress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr, out_len_ptr,
+                          status_ptr, nblocks, stream=0, js_compat=False, dict_ptr=None, dict_len=0):
+    _check(lib().lz4mi_decompress_blocks(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr,
+                                         dict_ptr, dict_len, out_len_ptr, status_ptr, nblocks,
+                                         DEVICE_PTRS | (JS_COMPAT if js_compat else 0), stream or None))
+
+
+def compress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_len_ptr, nblocks, stream=0):
+    _check(lib().lz4mi_compress_blocks(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_len_ptr, nblocks,
+                                       DEVICE_PTRS, stream or None))
+
+
+def xxh32_blocks_dev(in_ptr, off_ptr, len_ptr, hashes_ptr, nblocks, seed=0, stream=0, standard=False):
+    _check(lib().lz4mi_xxh32_blocks(in_ptr, off_ptr, len_ptr, seed & 0xFFFFFFFF, hashes_ptr, nblocks,
+                                    DEVICE_PTRS | (XXH_STANDARD if standard else 0), stream or None))
+
+
+def generate_blocks_dev(out_ptr, kind, seed0, block_size, nblocks, stream=0):
+    k = GENERATORS[kind] if isinstance(kind, str) else kind
+    _check(lib().lz4mi_generate_blocks(out_ptr, k, seed0, block_size, nblocks, stream or None))

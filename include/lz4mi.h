@@ -1,0 +1,147 @@
+/*
+ * include/lz4mi.h — C-ABI of the MI355X-native LZ4 block codec (liblz4mi.so).
+ *
+ * This is the drop-in boundary the reference's hot path is re-bound to. Each
+ * entry point names the reference interface it replaces (paths relative to the
+ * divortio-lz4 repository root). The N-API addon (divortio-lz4_amd/napi/) and
+ * the Python ctypes binding (divortio-lz4_amd/lz4mi/) are thin shims over it.
+ *
+ * Conventions
+ *  - Plain pointers and sizes; no framework types.
+ *  - By default every pointer is HOST memory: the call stages it to the GPU,
+ *    runs the kernel and copies results back before returning (synchronous,
+ *    like the reference's functions).
+ *  - With LZ4MI_DEVICE_PTRS every pointer (data AND the per-block descriptor
+ *    arrays) is DEVICE memory, the call only enqueues work on `stream`
+ *    (a hipStream_t; NULL = the library's per-device stream) and returns;
+ *    status/out_len are valid once the stream has been synchronised.
+ *  - Status codes: 0 = OK, negative = the reference's error (one per message,
+ *    see lz4mi_status_message), <= -100 = infrastructure failure.
+ */
+#ifndef LZ4MI_H
+#define LZ4MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (per block / per call) ------------------------------- */
+#define LZ4MI_OK 0
+#define LZ4MI_ERR_OUTPUT_TOO_SMALL (-1) /* "LZ4: Output Buffer Too Small"  src/block/blockDecompress.js:74 */
+#define LZ4MI_ERR_MALFORMED (-2)        /* "LZ4: Malformed Input"          src/block/blockDecompress.js:75 */
+#define LZ4MI_ERR_OFFSET0 (-3)          /* "LZ4: Invalid Offset 0"         src/block/blockDecompress.js:128 */
+#define LZ4MI_ERR_DICT_OOB (-4)         /* "LZ4: Dictionary Offset Out of Bounds" src/block/blockDecompress.js:150-152 */
+#define LZ4MI_ERR_MAGIC (-5)            /* "LZ4: Invalid Magic Number"     src/buffer/bufferDecompress.js:60 */
+#define LZ4MI_ERR_VERSION (-6)          /* "LZ4: Unsupported Version v"    src/buffer/bufferDecompress.js:67 */
+#define LZ4MI_ERR_CHECKSUM (-7)         /* "LZ4: Content Checksum Error"   src/buffer/bufferDecompress.js:216 */
+#define LZ4MI_ERR_RANGE (-8)            /* RangeError of TypedArray.set (stored block overflow) */
+#define LZ4MI_ERR_CROSS_BLOCK (-9)      /* batched decode only: a back-reference reaches before the block's
+                                           own output (not an independent block); the frame layer then
+                                           decodes the frame's blocks in order, one call per block */
+#define LZ4MI_ERR_HIP (-100)            /* a HIP runtime call failed */
+#define LZ4MI_ERR_ARG (-101)            /* invalid argument (size limits, NULL pointers) */
+#define LZ4MI_ERR_NO_DEVICE (-102)      /* no usable gfx950 device */
+
+/* ---- flags --------------------------------------------------------------- */
+#define LZ4MI_DEVICE_PTRS 0x1u   /* all pointers are device pointers; async on `stream` */
+#define LZ4MI_JS_COMPAT 0x2u     /* decode exactly like the reference JS decoder, including its
+                                    double-copy-tail rewrite. Default: LZ4 spec. */
+#define LZ4MI_XXH_STANDARD 0x4u  /* spec XXH32 lane convergence instead of the reference's variant */
+
+/* Largest block the kernels accept (the reference's largest block size is 4 MiB;
+ * raw calls may pass more, up to 2^31-1 like the reference's `|0` arithmetic). */
+#define LZ4MI_MAX_BLOCK 0x7FFFFFFFu
+
+/* Worst-case compressed size of an n-byte block (n + n/255 + 16). */
+static inline uint64_t lz4mi_compress_bound(uint64_t n) { return n + n / 255u + 16u; }
+
+/* Human-readable message of a status (the reference's exact error string). */
+const char* lz4mi_status_message(int32_t status);
+
+/* Device selection / info. Returns LZ4MI_OK or LZ4MI_ERR_*. */
+int32_t lz4mi_init(int32_t device);
+int32_t lz4mi_device_count(void);
+const char* lz4mi_version(void);
+
+/*
+ * Batched raw-block DECOMPRESS.
+ * Replaces: decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary)
+ *           src/block/blockDecompress.js:30-275 (exported as LZ4.decompressRaw, src/lz4.js:33),
+ *           and the per-block loop of decompressBuffer src/buffer/bufferDecompress.js:133-192.
+ * Block b reads in[in_off[b] .. +in_len[b]) and writes out[out_off[b] ..
+ * +out_cap[b]). Positions are absolute in `out` exactly as in the reference:
+ * a back-reference below out[out_off[b]] reads earlier bytes of `out`, and
+ * below out[0] reads the tail of `dict` (dict_len bytes, may be 0).
+ * out_len[b] = bytes produced (outPos - outputOffset); status[b] per block.
+ * With nblocks > 1 the blocks must be independent: a back-reference that
+ * reaches before the block's own output start yields LZ4MI_ERR_CROSS_BLOCK
+ * for that block (with nblocks == 1 it reads the preceding bytes of `out`,
+ * then `dict`, exactly as the reference). LZ4MI_JS_COMPAT decodes the blocks
+ * in order on one lane with the reference's byte-level behaviour.
+ * Returns LZ4MI_OK when the batch ran (per-block errors are in status[]).
+ */
+int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                const uint8_t* dict, uint32_t dict_len,
+                                uint32_t* out_len, int32_t* status, uint32_t nblocks, uint32_t flags,
+                                void* stream);
+
+/*
+ * Batched raw-block COMPRESS (fresh hash table per block: independent blocks).
+ * Replaces: compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset)
+ *           src/block/blockCompress.js:31-233 (LZ4.compressRaw, src/lz4.js:32) as called by
+ *           compressBuffer's block loop src/buffer/bufferCompress.js:209-239 with
+ *           blockIndependence=true. Output is byte-identical to the reference encoder.
+ * Block b compresses in[in_off[b] .. +in_len[b]) into out[out_off[b] ..), a slot of
+ * at least lz4mi_compress_bound(in_len[b]) bytes; out_len[b] = compressed size.
+ * The stored-block decision (bufferCompress.js:221-231) is the caller's.
+ */
+int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                              uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                              uint32_t nblocks, uint32_t flags, void* stream);
+
+/*
+ * Single raw-block COMPRESS with a caller-owned hash table (dependent blocks,
+ * dictionary prewarm, LZ4.compressRaw with a non-empty table).
+ * Replaces: compressBlock src/block/blockCompress.js:31-233 with full semantics:
+ * positions are absolute in src[0 .. src_total); the block is
+ * src[src_start .. +src_len); `table` (16384 int32, values = position+1, <=0 empty)
+ * is read and written back; output written at out[out_off ..) (out_total bytes
+ * available in out; writes past it are dropped, as with a typed array).
+ * Returns the number of bytes the reference would report written (>= 0) or a
+ * negative status.
+ */
+int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
+                                   int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off,
+                                   uint32_t flags, void* stream);
+
+/*
+ * XXH32, one buffer, on the host CPU (the frame content checksum is one serial
+ * chain). Replaces: xxHash32(input, seed) src/xxhash32/xxhash32.js:21-98.
+ * flags & LZ4MI_XXH_STANDARD selects the spec convergence.
+ */
+uint32_t lz4mi_xxh32(const uint8_t* data, size_t len, uint32_t seed, uint32_t flags);
+
+/*
+ * Batched XXH32 of independent buffers on the GPU (per-block checksums,
+ * dictionary ids, parity digests). hashes[b] = xxHash32(in[off[b] .. +len[b]), seed).
+ */
+int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
+                           uint32_t* hashes, uint32_t nblocks, uint32_t flags, void* stream);
+
+/*
+ * Synthetic input generator (bench/test support, not a reference interface):
+ * block b = generator `kind` with seed seed0 + b, block_size bytes each,
+ * written to out[b * block_size ..] (device pointer, async on stream).
+ * kind: 0 random, 1 repetitive (i % 251), 2 tiles216.
+ */
+int32_t lz4mi_generate_blocks(uint8_t* out, uint32_t kind, uint32_t seed0, uint32_t block_size,
+                              uint32_t nblocks, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZ4MI_H */

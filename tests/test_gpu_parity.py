@@ -1,0 +1,213 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the reference's
+golden vectors and the pinned CPU oracle. Bit-exact for every byte.
+
+Run on a real MI355X: python -m pytest tests -m gpu
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import cases_of, golden_bytes
+
+lz4mi = pytest.importorskip("lz4mi")
+
+pytestmark = pytest.mark.gpu
+
+MESSAGES = {
+    -1: "LZ4: Output Buffer Too Small",
+    -2: "LZ4: Malformed Input",
+    -3: "LZ4: Invalid Offset 0",
+    -4: "LZ4: Dictionary Offset Out of Bounds",
+}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    lz4mi.init(0)
+
+
+def _src_of(case):
+    if "gen" in case:
+        g = case["gen"]
+        return O.generate(g["gen"], g["seed"], g["n"])
+    return golden_bytes(case["src_file"]).copy()
+
+
+def test_compress_matches_reference_golden(manifest):
+    cases = cases_of(manifest, "block")
+    srcs = [_src_of(c) for c in cases]
+    comps = lz4mi.compress_blocks(srcs)          # one batched launch
+    for c, comp in zip(cases, comps):
+        assert comp.size == c["comp_len"], c["name"]
+        assert "%08x" % O.xxh32(comp) == c["comp_xxh"], c["name"]
+        if c["comp_file"]:
+            assert np.array_equal(comp, golden_bytes(c["comp_file"])), c["name"]
+
+
+def test_decompress_reference_blocks_spec_and_jscompat(manifest):
+    cases = cases_of(manifest, "block")
+    srcs = [_src_of(c) for c in cases]
+    comps = [O.compress_block_bytes(s) for s in srcs]
+    st, outs, lens = lz4mi.decompress_blocks(comps, [s.size for s in srcs])
+    for c, s, o, k, n in zip(cases, srcs, outs, st, lens):
+        assert k == 0 and n == s.size, c["name"]
+        assert np.array_equal(o, s), c["name"]
+    # js-compat: each block in its own output array, as the golden vectors were
+    # made (batched, a block's rewrite may legitimately touch its predecessor's tail)
+    res = [lz4mi.decompress_blocks([cb], [s.size], js_compat=True) for cb, s in zip(comps, srcs)]
+    st = [r[0][0] for r in res]
+    outs = [r[1][0] for r in res]
+    lens = [r[2][0] for r in res]
+    for c, s, o, k, n in zip(cases, srcs, outs, st, lens):
+        assert k == 0 and n == c["js_dec_written"], c["name"]
+        if c["js_dec_equals_input"]:
+            assert np.array_equal(o, s), c["name"]
+        else:
+            assert "%08x" % O.xxh32(o) == c["js_dec_xxh"], c["name"]
+
+
+def test_decode_edge_cases(manifest):
+    (g,) = cases_of(manifest, "decode_cases")
+    for c in g["cases"]:
+        for js in (False, True):
+            comp = np.array(c["comp"], dtype=np.uint8)
+            dic = None if c["dict"] is None else np.array(c["dict"], dtype=np.uint8)
+            out = np.zeros(c["out_len"], dtype=np.uint8)
+            if c["ok"]:
+                n = lz4mi.decompress_raw(comp, 0, comp.size, out, c["out_off"], dic, js_compat=js)
+                assert n == c["written"], (c["name"], js)
+                if js or c["name"] != "f1_trigger":
+                    assert out.tolist() == c["out"], (c["name"], js)
+            else:
+                with pytest.raises(lz4mi.Lz4miError) as ei:
+                    lz4mi.decompress_raw(comp, 0, comp.size, out, c["out_off"], dic, js_compat=js)
+                assert str(ei.value) == c["error"], (c["name"], js)
+
+
+def test_compress_raw_chain_with_table(manifest):
+    (c,) = cases_of(manifest, "block_chain")
+    g = c["gen"]
+    src = O.generate(g["gen"], g["seed"], g["n"])
+    out = np.zeros(400000, dtype=np.uint8)
+    table = np.full(16384, c["table_init"], dtype=np.int32)
+    pos = c["out_off0"]
+    for i, (start, n, expect) in enumerate(c["segments"]):
+        w = lz4mi.compress_raw(src, out, start, n, table, pos)
+        assert w == expect
+        pos += w
+        if i == 0:
+            assert np.array_equal(table.view(np.uint8), golden_bytes(c["table1_file"]))
+    assert np.array_equal(out[:pos], golden_bytes(c["out_file"]))
+    assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_final_file"]))
+
+
+def test_xxh32_batch_matches_reference(manifest):
+    (c,) = cases_of(manifest, "xxh32")
+    base = O.generate(c["input"]["gen"], c["input"]["seed"], c["input"]["n"])
+    rows = c["rows"]
+    h0 = lz4mi.xxh32_blocks([base[:n] for n, _, _ in rows], 0)
+    h1 = lz4mi.xxh32_blocks([base[:n] for n, _, _ in rows], 12345)
+    for (n, e0, e1), a, b in zip(rows, h0, h1):
+        assert "%08x" % a == e0 and "%08x" % b == e1, n
+        assert "%08x" % lz4mi.xxh32(base[:n]) == e0
+    hs = lz4mi.xxh32_blocks([base[:n] for n, _, _ in rows], 0, standard=True)
+    for (n, _, _), a in zip(rows, hs):
+        assert a == O.xxh32_std(base[:n])
+
+
+def test_generator_matches_oracle():
+    torch = pytest.importorskip("torch")
+    bs = 1 << 20
+    for kind in ("random", "repetitive", "tiles216"):
+        buf = torch.empty(3 * bs, dtype=torch.uint8, device="cuda")
+        lz4mi.generate_blocks_dev(buf.data_ptr(), kind, 5, bs, 3, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        host = buf.cpu().numpy()
+        for b in range(3):
+            assert np.array_equal(host[b * bs:(b + 1) * bs], O.generate(kind, 5 + b, bs)), (kind, b)
+
+
+def test_fuzz_roundtrip_and_corruption():
+    rng = np.random.default_rng(1234)
+    kinds = ["random", "repetitive", "tiles216", "copy", "runs", "text"]
+    srcs = []
+    for t in range(48):
+        n = int(rng.choice([0, 1, 5, 12, 13, 17, 100, 777, 4096, 20000, 65536, 100003, 300000]))
+        srcs.append(O.generate(kinds[t % len(kinds)], 100 + t, n))
+    comps = lz4mi.compress_blocks(srcs)
+    for s, c in zip(srcs, comps):
+        assert np.array_equal(c, O.compress_block_bytes(s))
+    st, outs, _ = lz4mi.decompress_blocks(comps, [s.size for s in srcs])
+    assert (st == 0).all()
+    for s, o in zip(srcs, outs):
+        assert np.array_equal(s, o)
+    # corrupted streams: status and (on success) bytes must equal the oracle's
+    bad, caps = [], []
+    for t, c in enumerate(comps):
+        c = c.copy()
+        if c.size:
+            for _ in range(1 + t % 4):
+                c[rng.integers(0, c.size)] = rng.integers(0, 256)
+        bad.append(c)
+        caps.append(srcs[t].size + (t % 3) * 7)
+    for js in (False, True):
+        if js:     # one output array per block (see test_decompress_reference_blocks_spec_and_jscompat)
+            res = [lz4mi.decompress_blocks([c], [k], js_compat=True) for c, k in zip(bad, caps)]
+            st = [r[0][0] for r in res]
+            outs = [r[1][0] for r in res]
+            lens = [r[2][0] for r in res]
+        else:
+            st, outs, lens = lz4mi.decompress_blocks(bad, caps)
+        for t, c in enumerate(bad):
+            est, ew, eo = O.decompress_block(c, caps[t], js_compat=js)
+            if st[t] == lz4mi.ERR_CROSS_BLOCK:         # batched: reaches before its own block
+                assert not js and est == lz4mi.ERR_DICT_OOB, t   # standalone at offset 0 that is OOB
+                continue
+            assert st[t] == est, (t, js)
+            if est == 0:
+                assert lens[t] == ew, (t, js)
+                assert np.array_equal(outs[t], eo[:min(ew, caps[t])]), (t, js)
+
+
+@pytest.mark.parametrize("kind", ["random", "repetitive", "tiles216"])
+def test_full_size_digest_manifest(manifest, kind):
+    """4 MiB blocks, all 16 reference seeds: generate, compress and decompress on
+    the GPU; compressed size and digests must equal the reference's."""
+    torch = pytest.importorskip("torch")
+    (g,) = cases_of(manifest, "digest_4mib")
+    rows = [r for r in g["rows"] if r["gen"] == kind]
+    n, bs = len(rows), rows[0]["n"]
+    seed0 = rows[0]["seed"]
+    assert [r["seed"] for r in rows] == list(range(seed0, seed0 + n))
+    dev, s = "cuda", torch.cuda.current_stream().cuda_stream
+    raw = torch.empty(n * bs, dtype=torch.uint8, device=dev)
+    lz4mi.generate_blocks_dev(raw.data_ptr(), kind, seed0, bs, n, s)
+    bound = lz4mi.compress_bound(bs)
+    slot = (bound + 255) & ~255
+    comp = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    in_off = torch.arange(n, dtype=torch.int64, device=dev) * bs
+    in_len = torch.full((n,), bs, dtype=torch.int32, device=dev)
+    out_off = torch.arange(n, dtype=torch.int64, device=dev) * slot
+    comp_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.compress_blocks_dev(raw.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), comp.data_ptr(),
+                              out_off.data_ptr(), comp_len.data_ptr(), n, s)
+    hashes = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.xxh32_blocks_dev(raw.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), hashes.data_ptr(), n, 0, s)
+    ch = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.xxh32_blocks_dev(comp.data_ptr(), out_off.data_ptr(), comp_len.data_ptr(), ch.data_ptr(), n, 0, s)
+    dec = torch.zeros(n * bs, dtype=torch.uint8, device=dev)
+    cap = torch.full((n,), bs, dtype=torch.int32, device=dev)
+    dlen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.decompress_blocks_dev(comp.data_ptr(), out_off.data_ptr(), comp_len.data_ptr(), dec.data_ptr(),
+                                in_off.data_ptr(), cap.data_ptr(), dlen.data_ptr(), st.data_ptr(), n, s)
+    dh = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.xxh32_blocks_dev(dec.data_ptr(), in_off.data_ptr(), dlen.data_ptr(), dh.data_ptr(), n, 0, s)
+    torch.cuda.synchronize()
+    for k, r in enumerate(rows):
+        assert "%08x" % (int(hashes[k]) & 0xFFFFFFFF) == r["src_xxh"], (kind, r["seed"])
+        assert int(comp_len[k]) == r["comp_len"], (kind, r["seed"])
+        assert "%08x" % (int(ch[k]) & 0xFFFFFFFF) == r["comp_xxh"], (kind, r["seed"])
+        assert int(st[k]) == 0 and int(dlen[k]) == bs
+        assert "%08x" % (int(dh[k]) & 0xFFFFFFFF) == r["js_dec_xxh"] == r["src_xxh"]
+    assert torch.equal(dec, raw)
