@@ -1,0 +1,25 @@
+// lz4mi_decompress.h — arguments shared by the decoder kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lz4mi {
+
+struct DecArgs {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    const uint32_t* in_len;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint32_t* out_cap;
+    const uint8_t* dict;
+    uint32_t dict_len;
+    uint32_t* out_len;
+    int32_t* status;
+    uint32_t nblocks;
+    int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
+};
+
+}  // namespace lz4mi
+
+extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream);

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Microbenchmark harness for kernel iteration (not the driver bench).
+
+Times lz4mi_decompress_blocks / compress / xxh32 on device-resident batches of
+4 MiB blocks for each generator; optionally loads alternative builds of the
+library (--so a.so b.so ...) and interleaves them in one process for A/B
+comparisons (cdna guide §5.4 rule 24).
+
+  python tools/microbench.py --gens tiles216,random,repetitive --blocks 4096 --reps 5
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "divortio-lz4_amd"))
+BLOCK = 4 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gens", default="tiles216,random,repetitive")
+    ap.add_argument("--blocks", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--so", nargs="*", default=[])
+    ap.add_argument("--what", default="decompress")
+    ap.add_argument("--skip-default", action="store_true", help="time only the --so libraries")
+    args = ap.parse_args()
+    import torch
+    import lz4mi
+    lz4mi.init(0)
+    libs = [] if args.skip_default else [("default", lz4mi.lib())]
+    for p in args.so:
+        L = ctypes.CDLL(os.path.abspath(p))
+        L.lz4mi_decompress_blocks.restype = ctypes.c_int32
+        L.lz4mi_decompress_blocks.argtypes = lz4mi.lib().lz4mi_decompress_blocks.argtypes
+        L.lz4mi_compress_blocks.restype = ctypes.c_int32
+        L.lz4mi_compress_blocks.argtypes = lz4mi.lib().lz4mi_compress_blocks.argtypes
+        L.lz4mi_init.restype = ctypes.c_int32
+        assert L.lz4mi_init(0) == 0
+        libs.append((os.path.basename(p), L))
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    sp = s.cuda_stream
+    n = args.blocks
+    res = {}
+    for gen in args.gens.split(","):
+        raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+        lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+        slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
+        comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+        roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
+        rlen = torch.full((n,), BLOCK, dtype=torch.int32, device="cuda")
+        coff = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+        clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+        lz4mi.compress_blocks_dev(raw.data_ptr(), roff.data_ptr(), rlen.data_ptr(), comp.data_ptr(),
+                                  coff.data_ptr(), clen.data_ptr(), n, sp)
+        dec = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+        dlen = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        cbytes = int(clen.sum())
+        for name, L in libs:
+            def run():
+                if args.what == "decompress":
+                    r = L.lz4mi_decompress_blocks(comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), dec.data_ptr(),
+                                                  roff.data_ptr(), rlen.data_ptr(), None, 0, dlen.data_ptr(),
+                                                  st.data_ptr(), n, 1, sp)
+                else:
+                    r = L.lz4mi_compress_blocks(raw.data_ptr(), roff.data_ptr(), rlen.data_ptr(), comp.data_ptr(),
+                                                coff.data_ptr(), clen.data_ptr(), n, 1, sp)
+                assert r == 0
+            run()
+            torch.cuda.synchronize()
+            times = []
+            for _ in range(args.reps):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                run()
+                e1.record(s)
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1) / 1e3)
+            ok = True
+            if args.what == "decompress":
+                ok = bool(torch.equal(dec, raw)) and bool((st == 0).all())
+            t = sorted(times)[len(times) // 2]
+            res[f"{gen}/{name}"] = {"ms": round(t * 1e3, 3), "GBps": round(n * BLOCK / t / 1e9, 1),
+                                    "hbm_frac": round((n * BLOCK + cbytes) / t / 8e12, 4), "ok": ok,
+                                    "ratio": round(n * BLOCK / cbytes, 3)}
+            print(gen, name, json.dumps(res[f"{gen}/{name}"]), flush=True)
+        del raw, comp, dec
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
