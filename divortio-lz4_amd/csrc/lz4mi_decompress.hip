@@ -8,7 +8,7 @@
 // reference's double-copy-tail rewrite.
 //
 // One wave64 per block, all 4096 blocks of a batch resident at once
-// (~9.9 KiB LDS, <= 128 VGPRs -> 16 waves per CU). Per 1 KiB chunk of the
+// (< 10 KiB LDS, <= 128 VGPRs -> 16 waves per CU). Per 1 KiB chunk of the
 // compressed stream:
 //  1. Stage it (+64 B lookahead) in LDS.
 //  2. next(p) of every position, branch-free (length fields of one extension
@@ -20,25 +20,30 @@
 //     whose left neighbour's exit is not on its walk re-walks from it. The
 //     result is the exact serial parse.
 //  4. Sequence table in LDS (literal source, lengths, offset, output start by
-//     wave prefix sums), errors in the reference's order, an output->sequence
-//     bucket map, and for every match its final source resolved once (through
-//     earlier sequences of the chunk down to a literal or to output finished
-//     by an earlier chunk).
-//  5. Output in 16-byte units aligned in the output address space, sequence-
-//     parallel: lane l takes sequence 64i+l and writes every unit whose first
-//     byte lies in it (a unit running into the next sequence takes its second
-//     source window from that sequence's entry), all loads in flight before
-//     the stores, 1 KiB per wave store instruction. Long sequences go to the
-//     whole wave; earlier output is read back from L2 (bypassing L1).
+//     wave prefix sums) and errors in the reference's order.
+//  5. Output, sequence-parallel (lane l takes sequence 64i+l), every run
+//     written with exact-width unaligned 16/8/4/2/1-byte pieces (the last
+//     16-byte piece of a run overlaps its predecessor instead of spilling),
+//     so lanes never touch each other's bytes:
+//       round 1: all literal runs (from LDS) and every match whose source
+//                lies entirely in output finished by earlier chunks;
+//       round r: after the previous round's stores are complete, every
+//                pending match whose source range meets no pending match.
+//     The earliest pending match is always ready, so the rounds terminate;
+//     on typical data two or three suffice. Matches are read straight from
+//     the output (L2, bypassing L1); an overlapping match (offset < length)
+//     is read through its period: a 16-byte window that wraps is merged from
+//     two loads, periods under 16 bytes are expanded in registers. Runs
+//     longer than 128 bytes are written by the whole wave.
 //  6. A sequence whose parse leaves the staged window (long literal runs or
 //     length varints: incompressible or highly repetitive data) is parsed from
-//     global memory with wave-wide 255-run scans and produced by the whole wave
-//     as a bulk literal copy and a bulk (possibly periodic) match copy.
+//     global memory with wave-wide 255-run scans and written by the whole
+//     wave, literal run first, then (after it is stored) the match run.
 #include "lz4mi_common.h"
 #include "lz4mi_decompress.h"
 
 #ifndef LZ4MI_ABLATE
-#define LZ4MI_ABLATE 0   // timing-only variant (tools/): 1 = parse + table only, no output
+#define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only
 #endif
 
 namespace lz4mi {
@@ -46,24 +51,30 @@ namespace lz4mi {
 constexpr int kChunk = 1024;                  // compressed bytes parsed per step
 constexpr int kPad = 64;                      // lookahead for sequences straddling the chunk end
 constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular sequence may touch
-constexpr int kStageWords = (kLim + 28) / 4;  // + 3-byte shift + 20-byte load window
+constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
 constexpr int kMaxSeq = kChunk / 3 + 4;       // every non-final sequence is >= 3 bytes
-constexpr int kBuckets = 1024;                // output -> sequence map granularity
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
-constexpr int kU = 2;                         // output units per lane in flight
-constexpr int kLaneUnits = 8;                 // sequences with more units are produced by the whole wave
+constexpr int kB = 2;                         // pieces per lane in flight
+constexpr int kLaneBytes = 128;               // longer runs are written by the whole wave
+constexpr int kShortPeriodBulk = 1024;        // longer runs of a < 16-byte period use the LDS phase table
 
 struct DecShared {
     uint32_t stage[kStageWords];
-    uint32_t t_out[kMaxSeq + 1];  // output start of each sequence (block-relative); [nseq] = table end
-    uint2 t_info[kMaxSeq + 1];    // {literal source (chunk-relative) | literal length << 16,
+    uint32_t t_out[kMaxSeq];      // output start of each sequence (block-relative)
+    uint2 t_info[kMaxSeq];        // {literal source (chunk-relative) | literal length << 16,
                                   //  match offset | match length << 16 (0: final literal-only sequence)}
-    uint32_t t_src[kMaxSeq + 1];  // final source of each match (pack_src)
-    uint16_t u2s[kLim];           // next-token table during the parse, then the bucket map
-    uint32_t unit[kWave * 4];     // per-lane 16-byte assembly slot / phase table
+    union {
+        uint16_t nxt[kLim];       // parse: next-token table
+        uint32_t pme[kLim / 2];   // output: ends of the pending matches
+    };
+    union {
+        uint32_t pms[kMaxSeq];    // output: starts of the pending matches
+        uint8_t pat[16 * 16];     // phase table of a long short-period run
+    };
 };
+static_assert(kLim / 2 >= kMaxSeq, "pending list must fit in the next-token table");
 
 struct Ctx {
     const uint8_t* blk;   // compressed block
@@ -74,13 +85,8 @@ struct Ctx {
     const uint8_t* dict;
     int32_t dict_len;
     int isolate;
-    int32_t mis;          // dst address mod 16 (units are aligned in the address space)
     int32_t ip;           // chunk start (block-relative compressed position)
-    uint32_t sh;          // staging shift
     int64_t O;            // output start of the current table (block-relative)
-    uint32_t nseq;
-    uint32_t shift;       // bucket = (y - O) >> shift
-    uint32_t nbk;
 };
 
 // ---------------------------------------------------------------- parsing
@@ -143,20 +149,6 @@ __device__ __forceinline__ SeqInfo seq_info(const DecShared& S, uint32_t k) {
     return SeqInfo{(int32_t)(v.x & 0xFFFF), (int32_t)(v.x >> 16), (int32_t)(v.y & 0xFFFF), (int32_t)(v.y >> 16)};
 }
 
-// Last sequence whose output start is <= y (y inside the table's output).
-__device__ __forceinline__ uint32_t seq_at(const Ctx& c, const DecShared& S, int32_t y) {
-    uint32_t b = (uint32_t)(y - (int32_t)c.O) >> c.shift;
-    if (b >= c.nbk) b = c.nbk - 1;
-    uint32_t s = S.u2s[b];
-    while (s + 1 < c.nseq && (int32_t)S.t_out[s + 1] <= y) ++s;
-    return s;
-}
-
-// ------------------------------------------------------------ byte access
-__device__ __forceinline__ uint32_t stage_byte(const DecShared& S, uint32_t idx) {
-    return ((const uint8_t*)S.stage)[idx];
-}
-
 // Byte of earlier output at block-relative position pos (dictionary below out[0]).
 __device__ __forceinline__ uint32_t hist_byte(const Ctx& c, int64_t pos) {
     int64_t abs = c.out_off + pos;
@@ -164,112 +156,142 @@ __device__ __forceinline__ uint32_t hist_byte(const Ctx& c, int64_t pos) {
     return c.dict ? c.dict[c.dict_len + abs] : 0u;
 }
 
-// ------------------------------------------------------ source resolution
-enum : uint32_t { K_HIST = 0, K_COMP = 1, K_GCOMP = 2, K_SLOW = 3 };
+// ------------------------------------------------------------------ runs
+// A run: n output bytes at y and where they come from.
+enum : uint32_t {
+    R_NONE = 0,
+    R_LDS = 1,    // literal bytes in the staged chunk (src = stage byte index)
+    R_COMP = 2,   // literal bytes in the compressed block in global memory (src = block position)
+    R_HIST = 3,   // match: earlier output (src = its block-relative position), read through `period`
+    R_BYTES = 4,  // match read byte by byte (dictionary, or within 16 bytes of a buffer edge)
+};
 
-// A contiguous source run: K_HIST = earlier output (block-relative position,
-// read back from L2), K_COMP = staged stream (LDS byte index), K_GCOMP =
-// compressed stream in global memory (block-relative position).
-struct Src {
-    int32_t pos;
-    int32_t m;
+struct Run {
+    int32_t y, n, src, period;   // period = match offset when the match overlaps itself, else 0
     uint32_t kind;
 };
 
-__device__ __forceinline__ uint32_t pack_src(uint32_t kind, int32_t pos) {
-    return (kind << 30) | ((uint32_t)pos & 0x3FFFFFFFu);
-}
-__device__ __forceinline__ uint32_t src_kind(uint32_t v) { return v >> 30; }
-__device__ __forceinline__ int32_t src_pos(uint32_t v) { return ((int32_t)(v << 2)) >> 2; }
+__device__ __forceinline__ Run no_run() { return Run{0, 0, 0, 0, R_NONE}; }
 
-// Can a 20-byte window be read at pos? (16 bytes + alignment slack)
-__device__ __forceinline__ bool window_ok(const Ctx& c, uint32_t kind, int32_t pos) {
-    if (kind == K_COMP) return pos >= 0;
-    if (kind == K_HIST) return c.out_off + pos >= 4 && pos + 20 <= c.cap;
-    return pos >= 4 && pos + 20 <= c.in_len;
+__device__ __forceinline__ Run shfl_run(const Run& R, int l) {
+    return Run{__shfl(R.y, l, kWave), __shfl(R.n, l, kWave), __shfl(R.src, l, kWave), __shfl(R.period, l, kWave),
+               (uint32_t)__shfl((int)R.kind, l, kWave)};
 }
 
-// Final source of the output run [y, y+m) of the current table, following
-// back-references through earlier sequences (periodic matches map straight
-// below their start); m shrinks to where the source stays contiguous.
-__device__ Src resolve(const Ctx& c, const DecShared& S, int32_t y, int32_t m) {
-    for (int d = 0; d < 16; ++d) {
-        if (y < (int32_t)c.O) {
-            if (m > (int32_t)c.O - y) m = (int32_t)c.O - y;
-            return Src{y, m, window_ok(c, K_HIST, y) ? K_HIST : K_SLOW};
-        }
-        uint32_t s = seq_at(c, S, y);
-        int32_t t0 = (int32_t)S.t_out[s];
-        int32_t rel = y - t0;
-        SeqInfo q = seq_info(S, s);
-        if (rel < q.ll) {
-            if (m > q.ll - rel) m = q.ll - rel;
-            return Src{(int32_t)c.sh + q.lit + rel, m, K_COMP};
-        }
-        int32_t mrel = rel - q.ll;
-        if (m > q.ml - mrel) m = q.ml - mrel;
-        int32_t r = mrel < q.off ? mrel : mrel % q.off;
-        if (m > q.off - r) m = q.off - r;
-        y = t0 + q.ll - q.off + r;
-    }
-    return Src{y, m, K_SLOW};
+// The match run of a sequence whose match starts at ms; n = 0 when nothing is
+// written (no match, or entirely past the capacity: the reference clips).
+__device__ __forceinline__ Run match_run(const Ctx& c, int32_t ms, int32_t off, int32_t ml) {
+    Run M{ms, 0, ms - off, off < ml ? off : 0, R_HIST};
+    if (ml == 0 || ms >= c.cap) return M;
+    M.n = (ms + ml > c.cap ? c.cap : ms + ml) - ms;
+    if (c.out_off + M.src < 16 || ms + 16 > c.cap) M.kind = R_BYTES;
+    return M;
+}
+// One past the last output byte a match run reads.
+__device__ __forceinline__ int32_t match_src_end(const Run& M) { return M.period ? M.y : M.src + M.n; }
+
+__device__ __forceinline__ int run_pieces(int32_t n) {
+    return n >= 16 ? (n + 15) >> 4 : (n <= 0 ? 0 : ((n & (n - 1)) == 0 ? 1 : 2));
 }
 
-// Source of the output run starting at y (at most `want` bytes) inside a
-// sequence (output start t0, fields q, packed match source sv).
-__device__ __forceinline__ Src seq_piece(const Ctx& c, int32_t t0, const SeqInfo& q, uint32_t sv, int32_t y,
-                                         int32_t want) {
-    const int32_t rel = y - t0;
-    if (rel < q.ll) return Src{(int32_t)c.sh + q.lit + rel, min(want, q.ll - rel), K_COMP};
-    const int32_t d = rel - q.ll;
-    uint32_t kind = src_kind(sv);
-    int32_t pos = src_pos(sv), m;
-    if (q.off >= q.ml) {
-        pos += d;
-        m = q.ml - d;
+// One store of a run: w bytes at y. mode 1 = window a, 2 = bytes [0, k) from
+// window a and the rest from window b (a period that wraps), 3 = period
+// `period` < w expanded from the 16 bytes at a starting at phase k,
+// 4 = byte-wise (a = run offset, b = source start).
+struct Piece {
+    int32_t y, a, b, k, period;
+    uint32_t w, mode, kind;
+};
+
+__device__ __forceinline__ Piece plan_piece(const Run& R, int p) {
+    Piece P{0, 0, 0, 16, 0, 16u, 0u, R.kind};
+    if (R.kind == R_NONE || p >= run_pieces(R.n)) return P;
+    int32_t d;
+    if (R.n >= 16) {
+        P.w = 16;
+        d = 16 * p < R.n - 16 ? 16 * p : R.n - 16;
     } else {
-        int32_t r = d < q.off ? d : d % q.off;
-        pos += r;
-        m = min(q.off - r, q.ml - d);
+        P.w = R.n >= 8 ? 8u : R.n >= 4 ? 4u : R.n >= 2 ? 2u : 1u;
+        d = p ? R.n - (int32_t)P.w : 0;
     }
-    if (kind == K_HIST && pos + 20 > c.cap) kind = K_SLOW;
-    return Src{pos, min(m, want), kind};
+    P.y = R.y + d;
+    P.period = R.period;
+    if (R.kind == R_BYTES) {
+        P.mode = 4;
+        P.a = d;
+        P.b = R.src;
+    } else if (R.period == 0) {
+        P.mode = 1;
+        P.a = R.src + d;
+    } else {
+        const int32_t per = R.period, r = d % per;
+        if (per < (int32_t)P.w) {
+            P.mode = 3;
+            P.a = R.src;
+            P.k = r;
+        } else if (r + (int32_t)P.w <= per) {
+            P.mode = 1;
+            P.a = R.src + r;
+        } else {
+            P.mode = 2;
+            P.a = R.src + r;
+            P.b = R.src + r - per;    // >= src - 15: match_run keeps 16 bytes of margin
+            P.k = per - r;
+        }
+    }
+    return P;
 }
 
-// Same, locating the sequence through the bucket map.
-__device__ __forceinline__ Src table_src(const Ctx& c, const DecShared& S, int32_t y, int32_t want) {
-    uint32_t s = seq_at(c, S, y);
-    return seq_piece(c, (int32_t)S.t_out[s], seq_info(S, s), S.t_src[s], y, want);
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// w bytes from an unaligned address (gfx950 runs in unaligned-access mode);
+// NT: bypass L1 (bytes this wave stored earlier in the launch).
+template <bool NT>
+__device__ __forceinline__ uint4 load_w(const uint8_t* p, uint32_t w) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (w == 16) {
+        if (NT) {
+            u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)p);
+            v = make_uint4(t.x, t.y, t.z, t.w);
+        } else {
+            __builtin_memcpy(&v, p, 16);
+        }
+    } else if (w == 8) {
+        if (NT) {
+            u32x2_t t = __builtin_nontemporal_load((const u32x2_t*)p);
+            v.x = t.x;
+            v.y = t.y;
+        } else {
+            __builtin_memcpy(&v, p, 8);
+        }
+    } else if (w == 4) {
+        if (NT) v.x = __builtin_nontemporal_load((const uint32_t*)p);
+        else __builtin_memcpy(&v.x, p, 4);
+    } else if (w == 2) {
+        uint16_t t;
+        if (NT) t = __builtin_nontemporal_load((const uint16_t*)p);
+        else __builtin_memcpy(&t, p, 2);
+        v.x = t;
+    } else {
+        v.x = NT ? (uint32_t)__builtin_nontemporal_load(p) : (uint32_t)*p;
+    }
+    return v;
 }
 
-// Bulk mapping (the one sequence a chunk could not hold): out[y] is source
-// byte base + phase, phase = y - lo, or (y - lo) mod period for a periodic match.
-struct Bulk {
-    uint32_t kind;
-    int32_t base, lo, period;
-};
-
-__device__ __forceinline__ Src bulk_src(const Ctx& c, const Bulk& B, int32_t y, int32_t want) {
-    int32_t d = y - B.lo;
-    int32_t r = B.period ? d % B.period : d;
-    int32_t m = B.period ? min(want, B.period - r) : want;
-    int32_t pos = B.base + r;
-    return Src{pos, m, window_ok(c, B.kind, pos) ? B.kind : K_SLOW};
-}
-
-__device__ __forceinline__ uint4 funnel4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4, uint32_t b) {
-    return make_uint4(funnel(d0, d1, b), funnel(d1, d2, b), funnel(d2, d3, b), funnel(d3, d4, b));
-}
-
-// 16 source bytes of a run. One code path for all kinds: a generic pointer
-// into the staged stream (LDS) or global memory, read as 5 aligned dwords
-// (non-temporal: output history is read from L2, never from a stale L1).
-__device__ __forceinline__ uint4 fetch16(const Ctx& c, const DecShared& S, const Src& r) {
-    const uint8_t* base = r.kind == K_COMP ? (const uint8_t*)S.stage : (r.kind == K_HIST ? (const uint8_t*)c.dst : c.blk);
-    uintptr_t a = (uintptr_t)(base + r.pos), a0 = a & ~(uintptr_t)3;
-    const uint32_t* q = (const uint32_t*)a0;
-    return funnel4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1), __builtin_nontemporal_load(q + 2),
-                   __builtin_nontemporal_load(q + 3), __builtin_nontemporal_load(q + 4), (uint32_t)(a - a0));
+__device__ __forceinline__ void store_w(uint8_t* p, uint4 v, uint32_t w) {
+    if (w == 16) {
+        __builtin_memcpy(p, &v, 16);
+    } else if (w == 8) {
+        __builtin_memcpy(p, &v, 8);
+    } else if (w == 4) {
+        __builtin_memcpy(p, &v.x, 4);
+    } else if (w == 2) {
+        uint16_t t = (uint16_t)v.x;
+        __builtin_memcpy(p, &t, 2);
+    } else {
+        *p = (uint8_t)v.x;
+    }
 }
 
 // bytes [0, k) from a, the rest from b
@@ -279,233 +301,113 @@ __device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, int32_t k) {
     uint32_t m = (1u << (8 * k)) - 1u;
     return (a & m) | (b & ~m);
 }
-
-// Unit alignment: units are 16-byte aligned in the address space of dst.
-__device__ __forceinline__ int32_t fl16(int32_t y, int32_t mis) { return ((y + mis) & ~15) - mis; }
-__device__ __forceinline__ int32_t cl16(int32_t y, int32_t mis) { return ((y + mis + 15) & ~15) - mis; }
-
-// Byte-wise unit (unit edges, runs that split more than once, dictionary
-// reads): resolved run by run, assembled in the lane's LDS slot.
-__device__ void unit_bytes(const Ctx& c, DecShared& S, int lane, int32_t y, int32_t n, bool bulk, const Bulk& B) {
-    uint8_t* ub = (uint8_t*)&S.unit[lane * 4];
-    int32_t k = 0;
-    while (k < n) {
-        int32_t yc = y + k, m = n - k;
-        uint32_t kind;
-        int64_t sp;
-        if (bulk) {
-            int32_t d = yc - B.lo;
-            int32_t r = B.period ? d % B.period : d;
-            if (B.period && B.period - r < m) m = B.period - r;
-            kind = B.kind;
-            sp = (int64_t)B.base + r;
-        } else {
-            for (;;) {
-                if (yc < (int32_t)c.O) {
-                    if (m > (int32_t)c.O - yc) m = (int32_t)c.O - yc;
-                    kind = K_HIST;
-                    sp = yc;
-                    break;
-                }
-                uint32_t s = seq_at(c, S, yc);
-                int32_t t0 = (int32_t)S.t_out[s];
-                int32_t rel = yc - t0;
-                SeqInfo q = seq_info(S, s);
-                if (rel < q.ll) {
-                    if (m > q.ll - rel) m = q.ll - rel;
-                    kind = K_COMP;
-                    sp = (int64_t)c.sh + q.lit + rel;
-                    break;
-                }
-                int32_t mrel = rel - q.ll;
-                if (m > q.ml - mrel) m = q.ml - mrel;
-                int32_t r = mrel < q.off ? mrel : mrel % q.off;
-                if (m > q.off - r) m = q.off - r;
-                yc = t0 + q.ll - q.off + r;
-            }
-        }
-        for (int32_t j = 0; j < m; ++j) {
-            uint32_t v;
-            if (kind == K_HIST) v = hist_byte(c, sp + j);
-            else if (kind == K_COMP) v = stage_byte(S, (uint32_t)(sp + j));
-            else v = (sp + j < c.in_len) ? c.blk[sp + j] : 0u;
-            ub[k + j] = (uint8_t)v;
-        }
-        k += m;
-    }
-    if (n == 16) {
-        *(uint4*)(c.dst + y) = *(const uint4*)&S.unit[lane * 4];
-    } else {
-        for (int32_t j = 0; j < n; ++j) c.dst[y + j] = ub[j];
-    }
+__device__ __forceinline__ uint4 pick4(uint4 a, uint4 b, int32_t k) {
+    return make_uint4(pick(a.x, b.x, k), pick(a.y, b.y, k - 4), pick(a.z, b.z, k - 8), pick(a.w, b.w, k - 12));
 }
 
-template <int N>
-__device__ __forceinline__ int32_t pick_slot(const int32_t (&a)[N], int j) {
-    int32_t v = a[0];
+// 16 bytes of a period per < 16 held in A[0, per), starting at phase r.
+__device__ __forceinline__ uint4 expand_period(uint4 A, int32_t r, int32_t per) {
+    uint32_t o[4] = {0, 0, 0, 0};
+    int32_t idx = r;
 #pragma unroll
-    for (int i = 1; i < N; ++i) v = j == i ? a[i] : v;
-    return v;
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t dw = idx < 4 ? A.x : idx < 8 ? A.y : idx < 12 ? A.z : A.w;
+        o[j >> 2] |= ((dw >> ((idx & 3) * 8)) & 255u) << ((j & 3) * 8);
+        idx = idx + 1 == per ? 0 : idx + 1;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-// Units prepared by the producers below: md 1 = one window, 2 = two windows
-// (bytes [0, A.m) from A, the rest from R), 3 = byte-wise.
-struct UnitBatch {
-    Src A[kU], R[kU];
-    int32_t y[kU], n[kU];
-    uint32_t md[kU];
-};
-
-__device__ __forceinline__ void plan_two(const Ctx& c, UnitBatch& U, int j) {
-    U.R[j].pos -= U.A[j].m;     // R's bytes land at unit offset A.m
-    if (U.R[j].kind != K_SLOW && U.A[j].m + U.R[j].m == 16 && window_ok(c, U.R[j].kind, U.R[j].pos)) U.md[j] = 2;
+__device__ __noinline__ void bytes_piece(const Ctx& c, int32_t y, int32_t a, int32_t src, uint32_t w, int32_t per) {
+    uint32_t o[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < w; ++j) {
+        const int32_t d = a + (int32_t)j;
+        const uint32_t v = hist_byte(c, (int64_t)src + (per ? d % per : d));
+        o[j >> 2] |= v << ((j & 3) * 8);
+    }
+    store_w(c.dst + y, make_uint4(o[0], o[1], o[2], o[3]), w);
 }
 
-// Load, merge and store a batch: every load is in flight before the first store.
-__device__ __forceinline__ void emit_units(const Ctx& c, DecShared& S, int lane, const UnitBatch& U, bool bulk,
-                                           const Bulk& B) {
-    uint4 va[kU], vb[kU];
+// Load, merge and store up to kB pieces: every load is in flight before the first store.
+__device__ __forceinline__ void emit(const Ctx& c, DecShared& S, const Piece (&P)[kB]) {
+    uint4 A[kB], B[kB];
 #pragma unroll
-    for (int j = 0; j < kU; ++j) {
-        if (U.md[j] == 1 || U.md[j] == 2) va[j] = fetch16(c, S, U.A[j]);
-        if (U.md[j] == 2) vb[j] = fetch16(c, S, U.R[j]);
-    }
-    uint32_t slow = 0;
-#pragma unroll
-    for (int j = 0; j < kU; ++j) {
-        if (U.md[j] == 1) {
-            *(uint4*)(c.dst + U.y[j]) = va[j];
-        } else if (U.md[j] == 2) {
-            int32_t k = U.A[j].m;
-            *(uint4*)(c.dst + U.y[j]) = make_uint4(pick(va[j].x, vb[j].x, k), pick(va[j].y, vb[j].y, k - 4),
-                                                   pick(va[j].z, vb[j].z, k - 8), pick(va[j].w, vb[j].w, k - 12));
+    for (int j = 0; j < kB; ++j) {
+        A[j] = make_uint4(0, 0, 0, 0);
+        B[j] = A[j];
+        if (P[j].mode >= 1 && P[j].mode <= 3) {
+            const uint32_t wa = P[j].mode == 3 ? 16u : P[j].w;
+            if (P[j].kind == R_LDS) A[j] = load_w<false>((const uint8_t*)S.stage + P[j].a, wa);
+            else if (P[j].kind == R_COMP) A[j] = load_w<false>(c.blk + P[j].a, wa);
+            else A[j] = load_w<true>(c.dst + P[j].a, wa);
         }
-        slow |= (U.md[j] == 3 ? 1u : 0u) << j;
+        if (P[j].mode == 2) B[j] = load_w<true>(c.dst + P[j].b, P[j].w);
     }
-    if (__ballot(slow != 0)) {
-        while (slow) {       // one call site for the byte-wise path
-            int j = __builtin_ctz(slow);
-            slow &= slow - 1;
-            unit_bytes(c, S, lane, pick_slot(U.y, j), pick_slot(U.n, j), bulk, B);
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+        if (P[j].mode >= 1 && P[j].mode <= 3) {
+            uint4 v = A[j];
+            if (P[j].mode == 2) v = pick4(A[j], B[j], P[j].k);
+            else if (P[j].mode == 3) v = expand_period(A[j], P[j].k, P[j].period);
+            store_w(c.dst + P[j].y, v, P[j].w);
+        } else if (P[j].mode == 4) {
+            bytes_piece(c, P[j].y, P[j].a, P[j].b, P[j].w, P[j].period);
         }
     }
 }
 
-// Whole-wave production of out[lo, hi): units spread over the lanes, each
-// unit's sources found through the table (or the Bulk mapping).
-__device__ void produce_units(const Ctx& c, DecShared& S, int lane, int32_t lo, int32_t hi, bool bulk, Bulk B) {
-    if (lo >= hi) return;
-    const int32_t y0 = fl16(lo, c.mis);
-    const uint32_t nunits = (uint32_t)(cl16(hi, c.mis) - y0) >> 4;
-    for (uint32_t u0 = lane; u0 < nunits; u0 += kWave * kU) {
-        UnitBatch U;
+// Each lane writes its own runs L then M (independent byte ranges).
+__device__ void lane_runs(const Ctx& c, DecShared& S, const Run& L, const Run& M) {
+    const int nl = L.kind == R_NONE ? 0 : run_pieces(L.n);
+    const int nt = nl + (M.kind == R_NONE ? 0 : run_pieces(M.n));
+    for (int q0 = 0; __ballot(q0 < nt) != 0; q0 += kB) {
+        Piece P[kB];
 #pragma unroll
-        for (int j = 0; j < kU; ++j) {
-            uint32_t u = u0 + kWave * j;
-            int32_t ua = y0 + 16 * (int32_t)u;
-            U.y[j] = ua < lo ? lo : ua;
-            U.n[j] = (ua + 16 > hi ? hi : ua + 16) - U.y[j];
-            U.md[j] = u < nunits ? 3u : 0u;
-            if (u < nunits && U.n[j] == 16) {
-                U.A[j] = bulk ? bulk_src(c, B, U.y[j], 16) : table_src(c, S, U.y[j], 16);
-                if (U.A[j].kind != K_SLOW) {
-                    if (U.A[j].m == 16) {
-                        U.md[j] = 1;
-                    } else {
-                        int32_t y2 = U.y[j] + U.A[j].m, w = 16 - U.A[j].m;
-                        U.R[j] = bulk ? bulk_src(c, B, y2, w) : table_src(c, S, y2, w);
-                        plan_two(c, U, j);
-                    }
-                }
-            }
+        for (int j = 0; j < kB; ++j) {
+            const int q = q0 + j;
+            const bool isl = q < nl;
+            const Run R{isl ? L.y : M.y, isl ? L.n : M.n, isl ? L.src : M.src, isl ? L.period : M.period,
+                        q < nt ? (isl ? L.kind : M.kind) : (uint32_t)R_NONE};
+            P[j] = plan_piece(R, isl ? q : q - nl);
         }
-        emit_units(c, S, lane, U, bulk, B);
+        emit(c, S, P);
     }
 }
 
-// Sequence-parallel production of the table: lane l takes sequence 64i+l and
-// writes the units whose first byte lies in it (sequence 0 also the partial
-// unit holding lo), at most kLaneUnits; longer sequences are flagged in
-// `longbits` (bit i) for the whole wave. All fields come from the sequence's
-// entry and the next one: no per-unit lookups.
-__device__ void produce_seqs(const Ctx& c, DecShared& S, int lane, int32_t lo, int32_t hi, uint32_t& longbits) {
-    const Bulk none{0, 0, 0, 0};
-    for (uint32_t i = 0; 64 * i < c.nseq; ++i) {
-        const uint32_t k = 64 * i + lane;
-        int32_t first = 0, nu = 0, t0 = 0, t1 = 0;
-        SeqInfo q{0, 0, 0, 0}, qn{0, 0, 0, 0};
-        uint32_t sv = 0, svn = 0;
-        if (k < c.nseq) {
-            t0 = (int32_t)S.t_out[k];
-            t1 = (int32_t)S.t_out[k + 1];
-            q = seq_info(S, k);
-            sv = S.t_src[k];
-            qn = seq_info(S, k + 1);
-            svn = S.t_src[k + 1];
-            first = k == 0 ? fl16(lo, c.mis) : cl16(t0, c.mis);
-            const int32_t t1c = t1 < hi ? t1 : hi;
-            nu = t1c > first ? (t1c - first + 15) >> 4 : 0;
-            if (nu > kLaneUnits) {
-                longbits |= 1u << i;
-                nu = 0;
-            }
-        }
-        for (int32_t j0 = 0; __ballot(j0 < nu) != 0; j0 += kU) {
-            UnitBatch U;
-#pragma unroll
-            for (int j = 0; j < kU; ++j) {
-                const int32_t u = first + 16 * (j0 + j);
-                U.md[j] = 0;
-                U.y[j] = u < lo ? lo : u;
-                U.n[j] = (u + 16 < hi ? u + 16 : hi) - U.y[j];
-                if (j0 + j < nu) {
-                    U.md[j] = 3;
-                    if (U.n[j] == 16) {
-                        U.A[j] = seq_piece(c, t0, q, sv, U.y[j], 16);
-                        if (U.A[j].kind != K_SLOW) {
-                            if (U.A[j].m == 16) {
-                                U.md[j] = 1;
-                            } else {
-                                const int32_t y2 = U.y[j] + U.A[j].m, w = 16 - U.A[j].m;
-                                U.R[j] = y2 < t1 ? seq_piece(c, t0, q, sv, y2, w) : seq_piece(c, t1, qn, svn, y2, w);
-                                plan_two(c, U, j);
-                            }
-                        }
-                    }
-                }
-            }
-            emit_units(c, S, lane, U, false, none);
-        }
-    }
-}
-
-// Periodic match with offset < 16 (long runs of a short pattern): the content
-// of a unit depends only on its phase; build the `off` phases once in LDS.
-__device__ __noinline__ void produce_short_period(const Ctx& c, DecShared& S, int lane, int32_t ms, int32_t hi,
-                                                  int32_t off) {
-    if (ms >= hi) return;
-    uint8_t* pat = (uint8_t*)S.unit;
-    const int32_t sb = ms - off;
+// Periodic run of period < 16 (long runs of a short pattern): the 16 bytes
+// at each phase are built once in LDS.
+__device__ __noinline__ void short_period_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+    const int32_t per = R.period;
     __syncthreads();
-    for (int idx = lane; idx < 16 * off; idx += kWave) {
-        int r = idx >> 4, j = idx & 15;
-        pat[idx] = (uint8_t)hist_byte(c, sb + (r + j) % off);
+    for (int idx = lane; idx < 16 * per; idx += kWave) {
+        const int r = idx >> 4, j = idx & 15;
+        S.pat[idx] = (uint8_t)hist_byte(c, (int64_t)R.src + (r + j) % per);
     }
     __syncthreads();
-    const int32_t y0 = fl16(ms, c.mis);
-    const uint32_t nunits = (uint32_t)(cl16(hi, c.mis) - y0) >> 4;
-    for (uint32_t u = lane; u < nunits; u += kWave) {
-        int32_t ua = y0 + 16 * (int32_t)u;
-        int32_t y = ua < ms ? ms : ua;
-        int32_t n = (ua + 16 > hi ? hi : ua + 16) - y;
-        int32_t r = (y - ms) % off;
-        if (n == 16) {
-            *(uint4*)(c.dst + y) = *(const uint4*)(pat + 16 * r);
-        } else {
-            for (int32_t j = 0; j < n; ++j) c.dst[y + j] = pat[16 * r + j];
-        }
+    const int np = run_pieces(R.n);   // R.n > kShortPeriodBulk: all pieces 16 bytes
+    for (int p = lane; p < np; p += kWave) {
+        const int32_t d = 16 * p < R.n - 16 ? 16 * p : R.n - 16;
+        uint4 v;
+        __builtin_memcpy(&v, S.pat + 16 * (d % per), 16);
+        __builtin_memcpy(c.dst + R.y + d, &v, 16);
     }
     __syncthreads();
+}
+
+// The whole wave writes one run.
+__device__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+    if (R.kind == R_NONE || R.n <= 0) return;
+    if (R.kind == R_HIST && R.period && R.period < 16 && R.n > kShortPeriodBulk) {
+        short_period_run(c, S, lane, R);
+        return;
+    }
+    const int np = run_pieces(R.n);
+    for (int p0 = 0; p0 < np; p0 += kWave * kB) {
+        Piece P[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) P[j] = plan_piece(R, p0 + lane + kWave * j);
+        emit(c, S, P);
+    }
 }
 
 // Wave-wide 255-run varint starting at block-relative q: returns the sum and
@@ -568,39 +470,34 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     c.dict = a.dict;
     c.dict_len = a.dict ? (int32_t)a.dict_len : 0;
     c.isolate = a.isolate;
-    c.mis = (int32_t)((uintptr_t)c.dst & 15);
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
 
     while (c.ip < c.in_len) {
-        // ---- 1. stage [ip, ip + kLim) ------------------------------------
+        // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads) ------------
         {
-            const uintptr_t A = (uintptr_t)(c.blk + c.ip), A0 = A & ~(uintptr_t)3;
-            c.sh = (uint32_t)(A - A0);
-            const int64_t rel0 = (int64_t)A0 - (int64_t)(uintptr_t)c.blk;
-            const bool inside = rel0 >= 0 && rel0 + 4 * kStageWords <= c.in_len;
-            for (int k = lane; k < kStageWords; k += kWave) {
-                const int64_t rel = rel0 + 4 * k;
-                uint32_t v;
-                if (inside) {
-                    v = *(const uint32_t*)(A0 + 4 * (uintptr_t)k);
+            uint8_t* st = (uint8_t*)S.stage;
+            for (int k = lane; k < kStageWords / 4; k += kWave) {
+                const int64_t r0 = (int64_t)c.ip + 16 * k;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (r0 + 16 <= c.in_len) {
+                    __builtin_memcpy(&v, c.blk + r0, 16);
                 } else {
-                    v = 0;
-                    for (int j = 0; j < 4; ++j) {
-                        int64_t r = rel + j;
-                        if (r >= 0 && r < c.in_len) v |= (uint32_t)c.blk[r] << (8 * j);
-                    }
+                    uint32_t o[4] = {0, 0, 0, 0};
+                    for (int j = 0; j < 16; ++j)
+                        if (r0 + j < c.in_len) o[j >> 2] |= (uint32_t)c.blk[r0 + j] << (8 * (j & 3));
+                    v = make_uint4(o[0], o[1], o[2], o[3]);
                 }
-                S.stage[k] = v;
+                __builtin_memcpy(st + 16 * k, &v, 16);
             }
         }
         __syncthreads();
-        const uint8_t* s = (const uint8_t*)S.stage + c.sh;
+        const uint8_t* s = (const uint8_t*)S.stage;
         const uint32_t rem = (uint32_t)(c.in_len - c.ip);
 
         // ---- 2. next-token table -----------------------------------------
-        uint16_t* nxt = S.u2s;   // the bucket map is built after the parse
+        uint16_t* nxt = S.nxt;
         for (uint32_t p = lane; p < (uint32_t)kLim; p += kWave) {
             bool slow;
             uint32_t v = next_fast(s, p, rem, slow);
@@ -610,6 +507,11 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             nxt[p] = (uint16_t)(v == kEnd ? 0xFFFEu : v == kStop ? 0xFFFFu : v);
         }
         __syncthreads();
+#if LZ4MI_ABLATE == 3
+        c.ip += kChunk;
+        __syncthreads();
+        continue;
+#endif
 
         // ---- 3. speculative walks + certification -------------------------
         const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
@@ -648,6 +550,11 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         const int last_lane = 63 - __builtin_clzll(has);
         const uint32_t last_tok = uniform(__shfl(seg0 + 31 - __builtin_clz(vis | 1u), last_lane, kWave));
         const bool cut = tail == kStop;
+#if LZ4MI_ABLATE == 2
+        c.ip = tail == kEnd ? c.in_len : c.ip + (cut ? kChunk : (int32_t)tail);
+        __syncthreads();
+        continue;
+#endif
 
         // ---- 4. sequence table -----------------------------------------
         const uint32_t cnt = __popc(vis) - ((cut && lane == last_lane) ? 1u : 0u);
@@ -688,48 +595,17 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         const uint32_t lincl = wave_incl_scan(run, lane);
         const uint32_t lbase = lincl - run;
         const int64_t total = uniform(__shfl(lincl, kWave - 1, kWave));
-        uint32_t shift = 4;
-        while ((total >> shift) >= kBuckets) ++shift;
-        c.shift = shift;
-        c.nbk = (uint32_t)((total + (1 << shift) - 1) >> shift);
-        if (c.nbk == 0) c.nbk = 1;
-        c.nseq = nseq;
         uint32_t first_err = 0xFFFFFFFFu;
         for (uint32_t k = base; k < base + cnt; ++k) {
-            const int64_t loc = (int64_t)lbase + S.t_out[k];
-            const int64_t os = c.O + loc;
+            const int64_t os = c.O + lbase + S.t_out[k];
             S.t_out[k] = (uint32_t)os;
             const SeqInfo q = seq_info(S, k);
             const uint32_t e = seq_error(c, os, (int64_t)c.ip + q.lit, q.ll, q.off, q.ml);
             if (e && first_err == 0xFFFFFFFFu) first_err = (k << 3) | e;
-            const int64_t B = 1ll << shift;
-            int64_t fb = (loc + B - 1) >> shift, lb = (loc + q.ll + q.ml + B - 1) >> shift;
-            if (lb > (int64_t)c.nbk) lb = c.nbk;
-            for (int64_t bq = fb; bq < lb; ++bq) S.u2s[bq] = (uint16_t)k;
-        }
-        if (lane == 0) {           // sentinel entry: the table's end
-            S.t_out[nseq] = (uint32_t)(c.O + total);
-            S.t_info[nseq] = make_uint2(0, 0);
-            S.t_src[nseq] = pack_src(K_SLOW, 0);
         }
         first_err = wave_min(first_err);
         __syncthreads();
         if (first_err != 0xFFFFFFFFu) { status = err_status(first_err & 7); break; }
-
-        // each match's final source, resolved once (sequence-parallel)
-        for (uint32_t k = lane; k < nseq; k += kWave) {
-            const SeqInfo q = seq_info(S, k);
-            uint32_t sv = pack_src(K_SLOW, 0);
-            const bool per = q.off < q.ml;
-            if (q.ml && (!per || q.off >= 16)) {     // shorter periods go byte-wise
-                const int32_t want = per ? q.off : q.ml;
-                const Src r = resolve(c, S, (int32_t)S.t_out[k] + q.ll - q.off, want);
-                if (r.kind != K_SLOW && r.m == want && r.pos < (1 << 29) && r.pos >= -(1 << 29))
-                    sv = pack_src(r.kind, r.pos);
-            }
-            S.t_src[k] = sv;
-        }
-        __syncthreads();
 
         // ---- 6. the sequence the window could not hold: parse it from memory
         int64_t cq = 0, cll = 0, cml = 0, clit = 0;
@@ -752,60 +628,85 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             cq = q;
         }
         const int64_t tab_hi = c.O + total;
-        const int64_t tab_end = tab_hi < (int64_t)c.cap ? tab_hi : (int64_t)c.cap;
 
-        // ---- 5. produce: table sequences lane-parallel, then (whole wave)
-        // the long ones, the cut sequence's literal run and, once everything
-        // below it is stored, its match run
-        uint32_t longbits = 0;
-#if LZ4MI_ABLATE != 1
-        if (nseq && c.O < tab_end) produce_seqs(c, S, lane, (int32_t)c.O, (int32_t)tab_end, longbits);
-#endif
-        uint64_t longlanes = __ballot(longbits != 0);
-        uint32_t lbits = 0;
-        int llane = 0;
-        int job = 0;     // 0 long table sequences, 1 cut literal, 2 cut match
-        while (job < 3) {
-            int64_t lo = 0, hi = 0;
-            const bool bulk = job > 0;
-            Bulk B{0, 0, 0, 0};
-            if (job == 0) {
-                if (lbits == 0) {
-                    if (longlanes == 0) { job = 1; continue; }
-                    llane = __builtin_ctzll(longlanes);
-                    longlanes &= longlanes - 1;
-                    lbits = uniform(__shfl(longbits, llane, kWave));
-                }
-                const uint32_t k = 64 * __builtin_ctz(lbits) + llane;
-                lbits &= lbits - 1;
-                const int32_t t0 = (int32_t)S.t_out[k], t1 = (int32_t)S.t_out[k + 1];
-                lo = k == 0 ? c.O : cl16(t0, c.mis);
-                hi = t1 < tab_end ? cl16(t1, c.mis) : tab_end;
-                if (hi > tab_end) hi = tab_end;
-            } else if (job == 1) {
-                job = 2;
-                if (!cut) break;
-                const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
-                if (e) { status = err_status(e); break; }
-                lo = tab_hi;
-                hi = tab_hi + cll;
-                B = Bulk{K_GCOMP, (int32_t)clit, (int32_t)lo, 0};
-            } else {
-                job = 3;
-                lo = tab_hi + cll;
-                hi = lo + cml;
-                if (cml == 0 || lo >= c.cap) break;
-                wait_vmem();    // everything below the match is read back as history
-                if ((int64_t)coff < cml && coff < 16) {
-                    produce_short_period(c, S, lane, (int32_t)lo, (int32_t)(hi < c.cap ? hi : c.cap), (int32_t)coff);
-                    break;
-                }
-                B = Bulk{K_HIST, (int32_t)(lo - coff), (int32_t)lo, (int64_t)coff < cml ? (int32_t)coff : 0};
+#if LZ4MI_ABLATE == 0
+        // ---- 5. output rounds ---------------------------------------------
+        uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
+        for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
+            const uint32_t k = 64 * i + lane;
+            Run L = no_run(), M = no_run();
+            if (k < nseq) {
+                const int32_t t0 = (int32_t)S.t_out[k];
+                const SeqInfo q = seq_info(S, k);
+                if (q.ll) L = Run{t0, q.ll, q.lit, 0, R_LDS};
+                M = match_run(c, t0 + q.ll, q.off, q.ml);
+                if (M.n == 0) M.kind = R_NONE;
+                else if (match_src_end(M) > (int32_t)c.O) { pend |= 1u << i; M.kind = R_NONE; }
             }
-            if (hi > c.cap) hi = c.cap;
-            if (lo < hi) produce_units(c, S, lane, (int32_t)lo, (int32_t)hi, bulk, B);
+            const bool longL = L.n > kLaneBytes, longM = M.kind != R_NONE && M.n > kLaneBytes;
+            lane_runs(c, S, longL ? no_run() : L, longM ? no_run() : M);
+            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
+            for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
         }
-        if (status) break;
+        for (;;) {                                             // rounds 2, 3, ...
+            uint32_t np = 0;
+            for (uint32_t i = 0; 64 * i < nseq; ++i) {
+                const bool pk = (pend >> i) & 1u;
+                const uint64_t bal = __ballot(pk);
+                if (pk) {
+                    const uint32_t k = 64 * i + lane;
+                    const uint32_t idx = np + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    const SeqInfo q = seq_info(S, k);
+                    const int32_t ms = (int32_t)S.t_out[k] + q.ll;
+                    S.pms[idx] = (uint32_t)ms;
+                    S.pme[idx] = (uint32_t)(ms + q.ml > c.cap ? c.cap : ms + q.ml);
+                }
+                np += (uint32_t)__popcll(bal);
+            }
+            if (np == 0) break;
+            __syncthreads();
+            wait_vmem();      // the previous round's stores are complete
+            for (uint32_t i = 0; 64 * i < nseq; ++i) {
+                if (__ballot((pend >> i) & 1u) == 0) continue;
+                Run M = no_run();
+                if ((pend >> i) & 1u) {
+                    const uint32_t k = 64 * i + lane;
+                    const SeqInfo q = seq_info(S, k);
+                    M = match_run(c, (int32_t)S.t_out[k] + q.ll, q.off, q.ml);
+                    // first pending match ending past the source start: ready if it starts at or past the source end
+                    const int32_t rs = M.src, re = match_src_end(M);
+                    uint32_t lo = 0, hi = np;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if ((int32_t)S.pme[mid] > rs) hi = mid;
+                        else lo = mid + 1;
+                    }
+                    if (lo >= np || (int32_t)S.pms[lo] >= re) pend &= ~(1u << i);
+                    else M.kind = R_NONE;
+                }
+                const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
+                lane_runs(c, S, no_run(), longM ? no_run() : M);
+                for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+            }
+            __syncthreads();
+        }
+        if (cut) {
+            const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
+            if (e) { status = err_status(e); break; }
+            wave_run(c, S, lane, Run{(int32_t)tab_hi, (int32_t)cll, (int32_t)clit, 0, cll ? (uint32_t)R_COMP : (uint32_t)R_NONE});
+            const Run M = match_run(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
+            if (M.n > 0) {
+                wait_vmem();    // everything below the match is read back as history
+                wave_run(c, S, lane, M);
+            }
+        }
+#else
+        if (cut) {
+            const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
+            if (e) { status = err_status(e); break; }
+        }
+#endif
         c.O = tab_hi;
         if (cut) {
             c.O += cll + cml;
