@@ -153,10 +153,11 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     int32_t st = ensure_init();
     if (st) return st;
     const int js = (flags & LZ4MI_JS_COMPAT) ? 1 : 0;
+    const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
         LZ4MI_TRY(lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
-                                          nblocks, js, pick_stream(stream)));
+                                          nblocks, mode, pick_stream(stream)));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_cap || !out_len || !status) return LZ4MI_ERR_ARG;
@@ -208,7 +209,7 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(lz4mi_launch_decompress(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off,
                                       m_out_cap, dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status,
-                                      nblocks, js, s));
+                                      nblocks, mode, s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
@@ -220,8 +221,11 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
         for (uint32_t b = 0; b < nblocks; ++b) {
             if (status[b] != 0) continue;
             uint64_t n = std::min<uint64_t>(out_len[b], out_cap[b]);
-            if (n) LZ4MI_TRY(hipMemcpyAsync(out + out_off[b], g_ctx.out.as<uint8_t>() + d_out_off[b], n,
-                                            hipMemcpyDeviceToHost, s));
+            // a lone block re-decoded reference-exactly may rewrite up to 7 bytes
+            // before its start (F1 at the block's first match): copy those back too
+            const uint64_t pre = (mode == 2 && nblocks == 1) ? std::min<uint64_t>(d_out_off[b], 8) : 0;
+            if (n + pre) LZ4MI_TRY(hipMemcpyAsync(out + out_off[b] - pre, g_ctx.out.as<uint8_t>() + d_out_off[b] - pre,
+                                                  n + pre, hipMemcpyDeviceToHost, s));
         }
     }
     LZ4MI_TRY(hipStreamSynchronize(s));

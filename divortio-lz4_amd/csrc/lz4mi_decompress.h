@@ -18,8 +18,13 @@ struct DecArgs {
     int32_t* status;
     uint32_t nblocks;
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
+    int f1check;   // flag blocks the reference's F1 rewrite would change (status kStatusF1)
 };
+
+constexpr int32_t kStatusF1 = -10;   // internal: block must be decoded by the serial reference-exact kernel
 
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream);
+// Re-decode, one block per workgroup, every block whose status is kStatusF1.
+extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream);

@@ -455,6 +455,22 @@ __device__ __forceinline__ uint32_t seq_error(const Ctx& c, int64_t out_start, i
 
 __device__ __forceinline__ int32_t err_status(uint32_t e) { return e == 5 ? -9 : -(int32_t)e; }
 
+// Would the reference's double-copy-tail rewrite (src/block/blockDecompress.js:219-250,
+// offset >= 8, length < 8, source in the output) change a byte of
+// this match's finished output? out[p] = out[p - off] for p in [ms + ml - 8, ms).
+// Reads bytes of this wave's completed output (after wait_vmem).
+// 0 = no change, 1 = changes (re-decode serially), 2 = the rewrite reads bytes
+// before the block's start: another block's output in a batch (reported as
+// LZ4MI_ERR_CROSS_BLOCK there, like any back-reference out of the block).
+__device__ __forceinline__ uint32_t f1_changes(const Ctx& c, int32_t ms, int32_t off, int32_t ml) {
+    if (ml == 0 || ml >= 8 || off < 8 || c.out_off + ms - off < 0) return 0;
+    const int32_t p0 = ms + ml - 8;
+    if (p0 - off < 0) return c.isolate ? 2u : 1u;
+    for (int32_t p = p0; p < ms && p < c.cap; ++p)
+        if (ld_nt_u8(c.dst + p) != ld_nt_u8(c.dst + p - off)) return 1;
+    return 0;
+}
+
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     __shared__ DecShared S;
     const int lane = threadIdx.x;
@@ -707,6 +723,17 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             if (e) { status = err_status(e); break; }
         }
 #endif
+        wait_vmem();        // this chunk's stores are complete before they are read back
+        if (a.f1check) {
+            uint32_t dv = 0;
+            for (uint32_t k = lane; k < nseq; k += kWave) {
+                const SeqInfo q = seq_info(S, k);
+                dv |= f1_changes(c, (int32_t)S.t_out[k] + q.ll, q.off, q.ml);
+            }
+            if (cut && lane == 0) dv |= f1_changes(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
+            if (__ballot(dv & 2u)) { status = -9; break; }
+            if (__ballot(dv)) { status = kStatusF1; break; }
+        }
         c.O = tab_hi;
         if (cut) {
             c.O += cll + cml;
@@ -716,7 +743,6 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         } else {
             c.ip += (int32_t)tail;
         }
-        wait_vmem();        // this chunk's stores are complete before the next chunk reads them back
         __syncthreads();
     }
     if (lane == 0) {
@@ -730,11 +756,14 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                               const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
-                                              int32_t* status, uint32_t nblocks, int js_compat, hipStream_t stream) {
+                                              int32_t* status, uint32_t nblocks, int mode, hipStream_t stream) {
+    // mode 0: LZ4 spec; 1: reference-exact serial kernel; 2: spec kernel + serial redo of F1 blocks
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
-                     nblocks > 1 ? 1 : 0};
+                     nblocks > 1 ? 1 : 0, mode == 2 ? 1 : 0};
     if (nblocks == 0) return hipSuccess;
-    if (js_compat) return lz4mi_launch_decompress_serial(a, stream);
+    if (mode == 1) return lz4mi_launch_decompress_serial(a, stream);
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || mode != 2) return e;
+    return lz4mi_launch_decompress_redo(a, stream);
 }

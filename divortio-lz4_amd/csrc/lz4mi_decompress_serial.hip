@@ -74,9 +74,20 @@ __global__ __launch_bounds__(64) void lz4mi_decompress_jscompat_kernel(DecArgs a
     for (uint32_t b = 0; b < a.nblocks; ++b) decode_block_jscompat(a, b);
 }
 
+__global__ __launch_bounds__(64) void lz4mi_decompress_redo_kernel(DecArgs a) {
+    const uint32_t b = blockIdx.x;
+    if (threadIdx.x != 0 || b >= a.nblocks || a.status[b] != kStatusF1) return;
+    decode_block_jscompat(a, b);
+}
+
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_jscompat_kernel, dim3(1), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_redo_kernel, dim3(a.nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }

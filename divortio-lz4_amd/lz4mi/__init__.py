@@ -24,6 +24,7 @@ ERR_HIP, ERR_ARG, ERR_NO_DEVICE = -100, -101, -102
 
 DEVICE_PTRS = 0x1
 JS_COMPAT = 0x2
+JS_EXACT = 0x8
 XXH_STANDARD = 0x4
 
 GEN_RANDOM, GEN_REPETITIVE, GEN_TILES216 = 0, 1, 2
@@ -160,8 +161,14 @@ def compress_raw(src, output, src_start, src_len, hash_table, output_offset):
     return int(r)
 
 
-def decompress_blocks(blocks, out_sizes, js_compat=False, dictionary=None):
-    """Independent compressed blocks -> (statuses, outputs) (GPU)."""
+def _dec_flags(js_compat, js_exact):
+    return JS_COMPAT if js_compat else (JS_EXACT if js_exact else 0)
+
+
+def decompress_blocks(blocks, out_sizes, js_compat=False, dictionary=None, js_exact=False):
+    """Independent compressed blocks -> (statuses, outputs) (GPU).
+    js_compat: the serial reference-exact kernel; js_exact: the parallel spec
+    kernel plus a serial re-decode of the blocks the reference's F1 rewrite changes."""
     arrs = [_u8(b) for b in blocks]
     n = len(arrs)
     in_len = np.array([a.size for a in arrs], dtype=np.uint32)
@@ -179,12 +186,13 @@ def decompress_blocks(blocks, out_sizes, js_compat=False, dictionary=None):
     d = _u8(dictionary)
     _check(lib().lz4mi_decompress_blocks(_p(src), _p(in_off), _p(in_len), _p(out), _p(out_off), _p(out_cap),
                                          _p(d), 0 if d is None else d.size, _p(out_len), _p(status), n,
-                                         JS_COMPAT if js_compat else 0, None))
+                                         _dec_flags(js_compat, js_exact), None))
     outs = [out[int(o):int(o) + min(int(l), int(c))].copy() for o, l, c in zip(out_off, out_len, out_cap)]
     return status, outs, out_len
 
 
-def decompress_raw(inp, input_offset, input_size, output, output_offset=0, dictionary=None, js_compat=False):
+def decompress_raw(inp, input_offset, input_size, output, output_offset=0, dictionary=None, js_compat=False,
+                   js_exact=False):
     """decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary):
     writes into `output` (numpy uint8) and returns bytes written; raises with the
     reference's message on error."""
@@ -200,7 +208,7 @@ def decompress_raw(inp, input_offset, input_size, output, output_offset=0, dicti
     seg = np.ascontiguousarray(seg) if seg.size else np.zeros(1, dtype=np.uint8)
     _check(lib().lz4mi_decompress_blocks(_p(seg), _p(in_off), _p(in_len), _p(output), _p(out_off), _p(out_cap),
                                          _p(d), 0 if d is None else d.size, _p(out_len), _p(status), 1,
-                                         JS_COMPAT if js_compat else 0, None))
+                                         _dec_flags(js_compat, js_exact), None))
     if status[0] != OK:
         raise Lz4miError(int(status[0]))
     return int(out_len[0])

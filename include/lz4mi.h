@@ -50,6 +50,10 @@ extern "C" {
 #define LZ4MI_JS_COMPAT 0x2u     /* decode exactly like the reference JS decoder, including its
                                     double-copy-tail rewrite. Default: LZ4 spec. */
 #define LZ4MI_XXH_STANDARD 0x4u  /* spec XXH32 lane convergence instead of the reference's variant */
+#define LZ4MI_JS_EXACT 0x8u      /* reference-exact result at spec-decoder speed: blocks are decoded by the
+                                    parallel spec kernel, which flags every block where the reference's
+                                    double-copy-tail rewrite (F1) would change a byte; only those blocks are
+                                    decoded again by the serial reference-exact kernel. */
 
 /* Largest block the kernels accept (the reference's largest block size is 4 MiB;
  * raw calls may pass more, up to 2^31-1 like the reference's `|0` arithmetic). */

@@ -66,6 +66,34 @@ def test_decompress_reference_blocks_spec_and_jscompat(manifest):
             assert "%08x" % O.xxh32(o) == c["js_dec_xxh"], c["name"]
 
 
+def test_decompress_js_exact_batched(manifest):
+    """JS_EXACT: the parallel spec kernel flags the blocks where the reference's
+    F1 rewrite changes bytes and re-decodes only those serially; one batch must
+    reproduce the reference decoder on every golden block (F1 blocks included)."""
+    cases = cases_of(manifest, "block")
+    srcs = [_src_of(c) for c in cases]
+    comps = [O.compress_block_bytes(s) for s in srcs]
+    st, outs, lens = lz4mi.decompress_blocks(comps, [s.size for s in srcs], js_exact=True)
+    for c, s, o, k, n in zip(cases, srcs, outs, st, lens):
+        if k == lz4mi.ERR_CROSS_BLOCK:
+            # the F1 rewrite of a match at the block's start reads bytes before the
+            # block (the predecessor's output in a shared buffer): batches report it,
+            # the caller decodes that block alone (below)
+            assert not c["js_dec_equals_input"], c["name"]
+            continue
+        assert k == 0 and n == c["js_dec_written"], c["name"]
+        if c["js_dec_equals_input"]:
+            assert np.array_equal(o, s), c["name"]
+        else:
+            assert "%08x" % O.xxh32(o) == c["js_dec_xxh"], c["name"]
+    # single-block calls (decompressRaw) agree too
+    for c, cb, s in zip(cases, comps, srcs):
+        out = np.zeros(max(1, s.size), dtype=np.uint8)
+        w = lz4mi.decompress_raw(cb, 0, cb.size, out, 0, js_exact=True)
+        assert w == c["js_dec_written"], c["name"]
+        assert "%08x" % O.xxh32(out[:s.size]) == (c["src_xxh"] if c["js_dec_equals_input"] else c["js_dec_xxh"]), c["name"]
+
+
 def test_decode_edge_cases(manifest):
     (g,) = cases_of(manifest, "decode_cases")
     for c in g["cases"]:
