@@ -43,10 +43,29 @@
 #include "lz4mi_decompress.h"
 
 #ifndef LZ4MI_ABLATE
-#define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only
+#define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
+                         // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
+#endif
+
+#ifndef LZ4MI_PROFILE
+#define LZ4MI_PROFILE 0  // timing-only variant (tools/): per-phase wall-clock accumulation
 #endif
 
 namespace lz4mi {
+
+#if LZ4MI_PROFILE
+__device__ unsigned long long g_prof[16];
+#define PROF(i)                              \
+    do {                                     \
+        const uint64_t t_ = wall_clock64();  \
+        prof[i] += t_ - prof_t;              \
+        prof_t = t_;                         \
+    } while (0)
+#define PROF_COUNT(i, n) (prof[i] += (n))
+#else
+#define PROF(i) ((void)0)
+#define PROF_COUNT(i, n) ((void)0)
+#endif
 
 constexpr int kChunk = 1024;                  // compressed bytes parsed per step
 constexpr int kPad = 64;                      // lookahead for sequences straddling the chunk end
@@ -335,6 +354,7 @@ __device__ __forceinline__ void emit(const Ctx& c, DecShared& S, const Piece (&P
     for (int j = 0; j < kB; ++j) {
         A[j] = make_uint4(0, 0, 0, 0);
         B[j] = A[j];
+        if (LZ4MI_ABLATE == 5) continue;
         if (P[j].mode >= 1 && P[j].mode <= 3) {
             const uint32_t wa = P[j].mode == 3 ? 16u : P[j].w;
             if (P[j].kind == R_LDS) A[j] = load_w<false>((const uint8_t*)S.stage + P[j].a, wa);
@@ -349,6 +369,10 @@ __device__ __forceinline__ void emit(const Ctx& c, DecShared& S, const Piece (&P
             uint4 v = A[j];
             if (P[j].mode == 2) v = pick4(A[j], B[j], P[j].k);
             else if (P[j].mode == 3) v = expand_period(A[j], P[j].k, P[j].period);
+            if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
+                if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pat[0] = 1;
+                continue;
+            }
             store_w(c.dst + P[j].y, v, P[j].w);
         } else if (P[j].mode == 4) {
             bytes_piece(c, P[j].y, P[j].a, P[j].b, P[j].w, P[j].period);
@@ -489,8 +513,13 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
+#if LZ4MI_PROFILE
+    uint64_t prof[16] = {0};
+    uint64_t prof_t = wall_clock64();
+#endif
 
     while (c.ip < c.in_len) {
+        PROF_COUNT(10, 1);
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads) ------------
         {
             uint8_t* st = (uint8_t*)S.stage;
@@ -512,6 +541,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         const uint8_t* s = (const uint8_t*)S.stage;
         const uint32_t rem = (uint32_t)(c.in_len - c.ip);
 
+        PROF(0);
         // ---- 2. next-token table -----------------------------------------
         uint16_t* nxt = S.nxt;
         for (uint32_t p = lane; p < (uint32_t)kLim; p += kWave) {
@@ -529,6 +559,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         continue;
 #endif
 
+        PROF(1);
         // ---- 3. speculative walks + certification -------------------------
         const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
         uint32_t vis = 0, x;
@@ -572,6 +603,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         continue;
 #endif
 
+        PROF(2);
         // ---- 4. sequence table -----------------------------------------
         const uint32_t cnt = __popc(vis) - ((cut && lane == last_lane) ? 1u : 0u);
         const uint32_t incl = wave_incl_scan(cnt, lane);
@@ -623,6 +655,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         __syncthreads();
         if (first_err != 0xFFFFFFFFu) { status = err_status(first_err & 7); break; }
 
+        PROF(3);
         // ---- 6. the sequence the window could not hold: parse it from memory
         int64_t cq = 0, cll = 0, cml = 0, clit = 0;
         uint32_t coff = 0;
@@ -645,7 +678,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         }
         const int64_t tab_hi = c.O + total;
 
-#if LZ4MI_ABLATE == 0
+#if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
+        PROF(4);
         // ---- 5. output rounds ---------------------------------------------
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
@@ -664,7 +698,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
         }
-        for (;;) {                                             // rounds 2, 3, ...
+        PROF(5);
+        for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
             uint32_t np = 0;
             for (uint32_t i = 0; 64 * i < nseq; ++i) {
                 const bool pk = (pend >> i) & 1u;
@@ -681,6 +716,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                 np += (uint32_t)__popcll(bal);
             }
             if (np == 0) break;
+            PROF_COUNT(11, 1);
             __syncthreads();
             wait_vmem();      // the previous round's stores are complete
             for (uint32_t i = 0; 64 * i < nseq; ++i) {
@@ -707,7 +743,9 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             }
             __syncthreads();
         }
+        PROF(6);
         if (cut) {
+            PROF_COUNT(12, 1);
             const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
             if (e) { status = err_status(e); break; }
             wave_run(c, S, lane, Run{(int32_t)tab_hi, (int32_t)cll, (int32_t)clit, 0, cll ? (uint32_t)R_COMP : (uint32_t)R_NONE});
@@ -723,6 +761,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             if (e) { status = err_status(e); break; }
         }
 #endif
+        PROF(7);
         wait_vmem();        // this chunk's stores are complete before they are read back
         if (a.f1check) {
             uint32_t dv = 0;
@@ -744,7 +783,12 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             c.ip += (int32_t)tail;
         }
         __syncthreads();
+        PROF(8);
     }
+#if LZ4MI_PROFILE
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
+#endif
     if (lane == 0) {
         a.status[b] = status;
         a.out_len[b] = status ? 0u : (uint32_t)c.O;
@@ -752,6 +796,15 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 }
 
 }  // namespace lz4mi
+
+#if LZ4MI_PROFILE
+// Per-phase wall-clock ticks (100 MHz) summed over all waves since the last call; resets.
+extern "C" int lz4mi_debug_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4mi::g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lz4mi::g_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,

@@ -1,0 +1,96 @@
+"""Multi-GPU sharding of independent LZ4 frame blocks.
+
+One process per GPU. Independent blocks need no exchange to be compressed or
+decoded: each rank takes its own range (`shard_range`). The frame is the one
+real exchange step: the compressed blocks of all ranks are concatenated, in
+block order, between the header and the EndMark. `gather_frame` does that with
+two collectives over `torch.distributed` (RCCL over xGMI with the nccl backend,
+gloo on CPU):
+
+  1. all-gather of each rank's record byte count (one int64 per rank);
+  2. all-gather of the records, padded to the largest rank's count.
+
+Each rank's records are already laid out exactly as the reference's block loop
+writes them (bufferCompress.js:209-239): LE32 size + payload when
+0 < compSize < blockSize, else LE32 (blockSize | 0x80000000) + the raw block.
+`frame_blocks` is the inverse walk for decoding (bufferDecompress.js:133-192).
+"""
+import numpy as np
+
+BLOCK_MAX_SIZES = {4: 65536, 5: 262144, 6: 1048576, 7: 4194304}
+
+
+def shard_range(nblocks, rank, world):
+    """Contiguous block range [lo, hi) of `rank`: ceil(N / world) blocks each."""
+    per = -(-nblocks // world)
+    lo = min(nblocks, rank * per)
+    return lo, min(nblocks, lo + per)
+
+
+def block_records(raw_blocks, comp_blocks):
+    """The frame bytes of consecutive blocks: size word + payload, stored fallback."""
+    parts = []
+    for raw, comp in zip(raw_blocks, comp_blocks):
+        n, c = int(raw.size), int(comp.size)
+        if 0 < c < n:
+            parts.append(np.array([c], dtype="<u4").view(np.uint8))
+            parts.append(np.asarray(comp, dtype=np.uint8))
+        else:
+            parts.append(np.array([(n | 0x80000000) & 0xFFFFFFFF], dtype="<u4").view(np.uint8))
+            parts.append(np.asarray(raw, dtype=np.uint8))
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+
+
+def gather_frame(local_records, header, trailer, group=None, device="cpu"):
+    """All ranks' block records in rank order, framed: header + records + EndMark + trailer.
+
+    local_records: uint8 numpy array (this rank's consecutive blocks, from block_records).
+    Returns the frame (numpy uint8) on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n = torch.tensor([int(local_records.size)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(1, max(sizes))
+    buf = torch.zeros(cap, dtype=torch.uint8, device=device)
+    if local_records.size:
+        buf[: local_records.size] = torch.from_numpy(np.ascontiguousarray(local_records)).to(device)
+    parts = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    body = [p[:s].cpu().numpy() for p, s in zip(parts, sizes)]
+    end = np.zeros(4, dtype=np.uint8)
+    return np.concatenate([np.frombuffer(bytes(header), dtype=np.uint8)] + body +
+                          [end, np.frombuffer(bytes(trailer), dtype=np.uint8)])
+
+
+def frame_blocks(frame):
+    """Walk a frame's blocks like the reference's decoder: returns (header_info, blocks)
+    with blocks = [(payload_pos, size, stored)] in order and the position after the EndMark."""
+    f = np.asarray(frame, dtype=np.uint8)
+    rd = lambda p: int(f[p]) | int(f[p + 1]) << 8 | int(f[p + 2]) << 16 | int(f[p + 3]) << 24 if p + 4 <= f.size else 0
+    if f.size < 4 or rd(0) != 0x184D2204:
+        raise ValueError("LZ4: Invalid Magic Number")
+    flg, bd = int(f[4]), int(f[5])
+    pos = 6
+    content_size = 0
+    if flg & 0x08:
+        content_size = rd(pos) + rd(pos + 4) * 4294967296
+        pos += 8
+    if flg & 0x01:
+        pos += 4
+    pos += 1
+    blocks = []
+    while pos < f.size:
+        bs = rd(pos)
+        pos += 4
+        if bs == 0:
+            break
+        n = bs & 0x7FFFFFFF
+        blocks.append((pos, n, bool(bs & 0x80000000)))
+        pos += n + (4 if flg & 0x10 else 0)
+    info = {"flg": flg, "independent": bool(flg & 0x20), "checksum": bool(flg & 0x04),
+            "content_size": content_size, "block_max": BLOCK_MAX_SIZES.get((bd >> 4) & 7, 4194304), "end": pos}
+    return info, blocks
