@@ -75,7 +75,9 @@ constexpr int kMaxSeq = kChunk / 3 + 4;       // every non-final sequence is >= 
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
-constexpr int kB = 2;                         // pieces per lane in flight
+constexpr int kB = 1;                         // pieces per lane per pipeline stage (lane-parallel runs)
+constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
+constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 128;               // longer runs are written by the whole wave
 constexpr int kShortPeriodBulk = 1024;        // longer runs of a < 16-byte period use the LDS phase table
 
@@ -347,54 +349,167 @@ __device__ __noinline__ void bytes_piece(const Ctx& c, int32_t y, int32_t a, int
     store_w(c.dst + y, make_uint4(o[0], o[1], o[2], o[3]), w);
 }
 
-// Load, merge and store up to kB pieces: every load is in flight before the first store.
-__device__ __forceinline__ void emit(const Ctx& c, DecShared& S, const Piece (&P)[kB]) {
-    uint4 A[kB], B[kB];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-        A[j] = make_uint4(0, 0, 0, 0);
-        B[j] = A[j];
-        if (LZ4MI_ABLATE == 5) continue;
-        if (P[j].mode >= 1 && P[j].mode <= 3) {
-            const uint32_t wa = P[j].mode == 3 ? 16u : P[j].w;
-            if (P[j].kind == R_LDS) A[j] = load_w<false>((const uint8_t*)S.stage + P[j].a, wa);
-            else if (P[j].kind == R_COMP) A[j] = load_w<false>(c.blk + P[j].a, wa);
-            else A[j] = load_w<true>(c.dst + P[j].a, wa);
-        }
-        if (P[j].mode == 2) B[j] = load_w<true>(c.dst + P[j].b, P[j].w);
+// A pipeline slot: one store of w bytes at y; mode 1 = window at a, 2 = bytes
+// [0, k) from the window at a, the rest from the window at a - per (a period
+// that wraps), 3 = period per < 16 expanded from the window at a from phase k.
+// Windows are always 16 bytes (match_run / the staging slack keep them in bounds).
+struct Slot {
+    int32_t y, a, k, per;
+    uint32_t wm;     // width | mode << 8
+};
+
+__device__ __forceinline__ Slot no_slot() { return Slot{0, 0, 0, 0, 0u}; }
+
+// Slot of piece p of run R (R is not R_BYTES; wrapping periods only when TWO).
+__device__ __forceinline__ Slot slot_of(const Run& R, int p) {
+    const Piece P = plan_piece(R, p);
+    return Slot{P.y, P.a, P.k, P.period, P.mode ? (P.w | (P.mode << 8)) : 0u};
+}
+template <uint32_t KIND>
+__device__ __forceinline__ uint4 load16(const Ctx& c, const DecShared& S, int32_t a) {
+    uint4 v;
+    if (KIND == R_LDS) {
+        __builtin_memcpy(&v, (const uint8_t*)S.stage + a, 16);
+    } else if (KIND == R_COMP) {
+        __builtin_memcpy(&v, c.blk + a, 16);
+    } else {
+        const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(c.dst + a));
+        v = make_uint4(t.x, t.y, t.z, t.w);
     }
+    return v;
+}
+
+template <uint32_t KIND, bool TWO, int NB>
+__device__ __forceinline__ void load_slots(const Ctx& c, const DecShared& S, const Slot (&s)[NB], uint4 (&A)[NB],
+                                           uint4 (&B)[NB]) {
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-        if (P[j].mode >= 1 && P[j].mode <= 3) {
-            uint4 v = A[j];
-            if (P[j].mode == 2) v = pick4(A[j], B[j], P[j].k);
-            else if (P[j].mode == 3) v = expand_period(A[j], P[j].k, P[j].period);
-            if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
-                if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pat[0] = 1;
-                continue;
-            }
-            store_w(c.dst + P[j].y, v, P[j].w);
-        } else if (P[j].mode == 4) {
-            bytes_piece(c, P[j].y, P[j].a, P[j].b, P[j].w, P[j].period);
-        }
+    for (int j = 0; j < NB; ++j) {
+        if (LZ4MI_ABLATE == 5) { A[j] = make_uint4(0, 0, 0, 0); B[j] = A[j]; continue; }
+        if (s[j].wm >> 8) A[j] = load16<KIND>(c, S, s[j].a);
+        if (TWO && (s[j].wm >> 8) == 2) B[j] = load16<KIND>(c, S, s[j].a - s[j].per);
     }
 }
 
-// Each lane writes its own runs L then M (independent byte ranges).
-__device__ void lane_runs(const Ctx& c, DecShared& S, const Run& L, const Run& M) {
-    const int nl = L.kind == R_NONE ? 0 : run_pieces(L.n);
-    const int nt = nl + (M.kind == R_NONE ? 0 : run_pieces(M.n));
-    for (int q0 = 0; __ballot(q0 < nt) != 0; q0 += kB) {
-        Piece P[kB];
+template <bool TWO, int NB>
+__device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Slot (&s)[NB], const uint4 (&A)[NB],
+                                            const uint4 (&B)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const uint32_t mode = s[j].wm >> 8;
+        if (!mode) continue;
+        uint4 v = A[j];
+        if (TWO && mode == 2) v = pick4(A[j], B[j], s[j].k);
+        else if (mode == 3) v = expand_period(A[j], s[j].k, s[j].per);
+        if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
+            if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pat[0] = 1;
+            continue;
+        }
+        const uint32_t w = s[j].wm & 255u;
+        if (w == 16) __builtin_memcpy(c.dst + s[j].y, &v, 16);
+        else store_w(c.dst + s[j].y, v, w);
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ bool any_slot(const Slot (&s)[NB]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) m |= s[j].wm;
+    return m != 0;
+}
+
+// Software-pipelined copy: the loads of stage n+1 are issued before the stores
+// of stage n, so no load waits behind a store it does not depend on (gfx9
+// counts loads and stores in one in-order vmcnt). Gen::fill(Slot (&)[kB])
+// hands out this lane's next pieces (sources already complete).
+template <uint32_t KIND, bool TWO, int NB, class Gen>
+__device__ __forceinline__ void pipe(const Ctx& c, DecShared& S, Gen& g) {
+    Slot s0[NB], s1[NB];
+    uint4 a0[NB], b0[NB], a1[NB], b1[NB];
+    g.fill(s0);
+    load_slots<KIND, TWO, NB>(c, S, s0, a0, b0);
+    for (;;) {
+        if (!__ballot(any_slot<NB>(s0))) break;
+        g.fill(s1);
+        load_slots<KIND, TWO, NB>(c, S, s1, a1, b1);
+        store_slots<TWO, NB>(c, S, s0, a0, b0);
+        if (!__ballot(any_slot<NB>(s1))) break;
+        g.fill(s0);
+        load_slots<KIND, TWO, NB>(c, S, s0, a0, b0);
+        store_slots<TWO, NB>(c, S, s1, a1, b1);
+    }
+}
+
+// Pieces of the whole wave over one run: piece p0 + lane + 64 j.
+template <int NB>
+struct WaveGen {
+    Run R;
+    int np, p0, lane;
+    __device__ __forceinline__ void fill(Slot (&s)[NB]) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int p = p0 + lane + kWave * j;
+            s[j] = p < np ? slot_of(R, p) : no_slot();
+        }
+        p0 += kWave * NB;
+    }
+};
+
+// Pieces of each lane's own non-periodic match runs from earlier output:
+// sequences 64 i + lane for every bit i of `bits` (every piece a single window).
+struct LaneMatchGen {
+    const Ctx& c;
+    const DecShared& S;
+    uint32_t bits;
+    int lane, q, np;
+    int32_t y, n, src;
+    __device__ __forceinline__ void fill(Slot (&s)[kB]) {
 #pragma unroll
         for (int j = 0; j < kB; ++j) {
-            const int q = q0 + j;
-            const bool isl = q < nl;
-            const Run R{isl ? L.y : M.y, isl ? L.n : M.n, isl ? L.src : M.src, isl ? L.period : M.period,
-                        q < nt ? (isl ? L.kind : M.kind) : (uint32_t)R_NONE};
-            P[j] = plan_piece(R, isl ? q : q - nl);
+            while (q >= np && bits) {
+                const uint32_t k = 64u * __builtin_ctz(bits) + lane;
+                bits &= bits - 1;
+                const SeqInfo qi = seq_info(S, k);
+                const Run M = match_run(c, (int32_t)S.t_out[k] + qi.ll, qi.off, qi.ml);
+                y = M.y;
+                n = M.n;
+                src = M.src;
+                np = run_pieces(n);
+                q = 0;
+            }
+            if (q < np) {
+                uint32_t w = 16;
+                int32_t d;
+                if (n >= 16) {
+                    d = 16 * q < n - 16 ? 16 * q : n - 16;
+                } else {
+                    w = n >= 8 ? 8u : 4u;             // match runs are >= 4 bytes
+                    d = q ? n - (int32_t)w : 0;
+                }
+                s[j] = Slot{y + d, src + d, 16, 0, w | (1u << 8)};
+            } else {
+                s[j] = no_slot();
+            }
+            ++q;
         }
-        emit(c, S, P);
+    }
+};
+
+// A lane's match run the pipeline does not take (periodic, or byte-wise near a
+// buffer edge / in the dictionary): piece by piece.
+__device__ __noinline__ void lane_slow_run(const Ctx& c, const DecShared& S, const Run& R) {
+    const int np = run_pieces(R.n);
+    for (int p = 0; p < np; ++p) {
+        const Piece P = plan_piece(R, p);
+        if (P.mode == 4) {
+            bytes_piece(c, P.y, P.a, P.b, P.w, P.period);
+            continue;
+        }
+        const uint4 A = load16<R_HIST>(c, S, P.a);
+        uint4 v = A;
+        if (P.mode == 2) v = pick4(A, load16<R_HIST>(c, S, P.b), P.k);
+        else if (P.mode == 3) v = expand_period(A, P.k, P.period);
+        store_w(c.dst + P.y, v, P.w);
     }
 }
 
@@ -418,19 +533,43 @@ __device__ __noinline__ void short_period_run(const Ctx& c, DecShared& S, int la
     __syncthreads();
 }
 
-// The whole wave writes one run.
-__device__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+// The whole wave writes one run (uniform R).
+__device__ __noinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
     if (R.kind == R_NONE || R.n <= 0) return;
     if (R.kind == R_HIST && R.period && R.period < 16 && R.n > kShortPeriodBulk) {
         short_period_run(c, S, lane, R);
         return;
     }
     const int np = run_pieces(R.n);
-    for (int p0 = 0; p0 < np; p0 += kWave * kB) {
-        Piece P[kB];
-#pragma unroll
-        for (int j = 0; j < kB; ++j) P[j] = plan_piece(R, p0 + lane + kWave * j);
-        emit(c, S, P);
+    if (R.kind == R_BYTES) {
+        for (int p = lane; p < np; p += kWave) {
+            const Piece P = plan_piece(R, p);
+            bytes_piece(c, P.y, P.a, P.b, P.w, P.period);
+        }
+        return;
+    }
+    if (R.period) {
+        WaveGen<kWaveB2> g{R, np, 0, lane};
+        pipe<R_HIST, true, kWaveB2>(c, S, g);
+        return;
+    }
+    WaveGen<kWaveB> g{R, np, 0, lane};
+    if (R.kind == R_LDS) pipe<R_LDS, false, kWaveB>(c, S, g);
+    else if (R.kind == R_COMP) pipe<R_COMP, false, kWaveB>(c, S, g);
+    else pipe<R_HIST, false, kWaveB>(c, S, g);
+}
+
+// Each lane copies its own short literal runs (LDS -> output; no vector-memory loads).
+__device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L) {
+    const int np = L.kind == R_NONE ? 0 : run_pieces(L.n);
+    for (int q = 0; __ballot(q < np) != 0; q += 2) {
+        const Piece P0 = plan_piece(L, q < np ? q : np), P1 = plan_piece(L, q + 1 < np ? q + 1 : np);
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+        if (P0.mode) __builtin_memcpy(&v0, (const uint8_t*)S.stage + P0.a, 16);
+        if (P1.mode) __builtin_memcpy(&v1, (const uint8_t*)S.stage + P1.a, 16);
+        if (LZ4MI_ABLATE == 4) continue;
+        if (P0.mode) store_w(c.dst + P0.y, v0, P0.w);
+        if (P1.mode) store_w(c.dst + P1.y, v1, P1.w);
     }
 }
 
@@ -682,6 +821,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         PROF(4);
         // ---- 5. output rounds ---------------------------------------------
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
+        uint32_t ready = 0;   // bit i: ... is written by this lane in this round
         for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
             const uint32_t k = 64 * i + lane;
             Run L = no_run(), M = no_run();
@@ -694,9 +834,16 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                 else if (match_src_end(M) > (int32_t)c.O) { pend |= 1u << i; M.kind = R_NONE; }
             }
             const bool longL = L.n > kLaneBytes, longM = M.kind != R_NONE && M.n > kLaneBytes;
-            lane_runs(c, S, longL ? no_run() : L, longM ? no_run() : M);
+            const bool fastM = M.kind == R_HIST && M.period == 0;
+            if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
+            lane_literals(c, S, longL ? no_run() : L);
+            if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
             for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+        }
+        {
+            LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
+            pipe<R_HIST, false, kB>(c, S, g);
         }
         PROF(5);
         for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
@@ -719,6 +866,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             PROF_COUNT(11, 1);
             __syncthreads();
             wait_vmem();      // the previous round's stores are complete
+            ready = 0;
             for (uint32_t i = 0; 64 * i < nseq; ++i) {
                 if (__ballot((pend >> i) & 1u) == 0) continue;
                 Run M = no_run();
@@ -738,8 +886,14 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                     else M.kind = R_NONE;
                 }
                 const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
-                lane_runs(c, S, no_run(), longM ? no_run() : M);
+                const bool fastM = M.kind == R_HIST && M.period == 0;
+                if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
+                if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+            }
+            {
+                LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
+                pipe<R_HIST, false, kB>(c, S, g);
             }
             __syncthreads();
         }
