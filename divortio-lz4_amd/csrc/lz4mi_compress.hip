@@ -222,6 +222,260 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Batch encoder (fresh table per block): the same parse, 4 blocks per CU.
+//
+// Table: a block's positions fit 22 bits, but a candidate only matters while
+// it is < 65536 bytes back, so each entry keeps the position's low 16 bits plus
+// a 2-bit code of its 32 KiB epoch (epoch mod 4): epochs g-2..g decode
+// uniquely, code (g+1) mod 4 means empty/stale, and entering epoch g relabels
+// the fields still carrying code g mod 4 (4 epochs old) as stale. 36 KiB
+// instead of 64 KiB; exact (the distance check still runs on the decoded position).
+//
+// Probing: up to 64 consecutive probes of the miss chain (positions i + the
+// prefix sum of the skip steps c >> 6) are evaluated at once, one per lane:
+// hash, table read, candidate verification. Every probe up to and including
+// the first hit happens in the reference, in order, each inserting its own
+// position; a batch is cut before the first lane whose hash repeats an
+// earlier lane's (found by writing lane ids into the table and reading them
+// back), so the batch's inserts never interact and the result is the serial one.
+//
+// Output goes to a 4 KiB LDS ring flushed in 16-byte units; long literal runs
+// are copied global -> global directly. No vector-memory store precedes the
+// next probe's loads except at ring flushes.
+constexpr int kCodeWords = 16384 / 16;
+constexpr int kRing = 4096;
+constexpr int kRingMask = kRing - 1;
+constexpr int32_t kDirectLit = 2048;   // longer literal runs bypass the ring
+
+struct FastShared {
+    uint16_t lo[16384];
+    uint32_t code[kCodeWords];
+    uint8_t ring[kRing];
+};
+
+struct FastOut {
+    uint8_t* dst;
+    int64_t op, flushed;   // flushed is 16-aligned except after the final flush
+};
+
+__device__ __forceinline__ uint32_t ld_u32(const CompJob& j, int64_t p) {
+    if (p >= 0 && (uint64_t)p + 4 <= j.src_total) {
+        uint32_t v;
+        __builtin_memcpy(&v, j.src + p, 4);
+        return v;
+    }
+    return src_byte(j, p) | (src_byte(j, p + 1) << 8) | (src_byte(j, p + 2) << 16) | (src_byte(j, p + 3) << 24);
+}
+
+// ring [flushed, floor16(op)) -> dst
+__device__ void ring_flush(FastShared& F, FastOut& o, int lane) {
+    const int64_t upto = o.op & ~(int64_t)15;
+    for (int64_t p = o.flushed + 16 * lane; p < upto; p += 16 * kWave) {
+        uint4 v;
+        __builtin_memcpy(&v, F.ring + (p & kRingMask), 16);
+        __builtin_memcpy(o.dst + p, &v, 16);
+    }
+    if (upto > o.flushed) o.flushed = upto;
+}
+
+__device__ __forceinline__ void ring_reserve(FastShared& F, FastOut& o, int lane, int64_t n) {
+    if (o.op + n - o.flushed > kRing) ring_flush(F, o, lane);
+}
+
+// n bytes of value v (n <= kRing - 16 per call)
+__device__ void ring_fill(FastShared& F, FastOut& o, int lane, int64_t n, uint32_t v) {
+    while (n > 0) {
+        const int64_t k = n < kRing - 16 ? n : kRing - 16;
+        ring_reserve(F, o, lane, k);
+        for (int64_t t = lane; t < k; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)v;
+        o.op += k;
+        n -= k;
+    }
+}
+
+__device__ __forceinline__ void ring_put(FastShared& F, FastOut& o, int lane, uint32_t v) {
+    ring_reserve(F, o, lane, 1);
+    if (lane == 0) F.ring[o.op & kRingMask] = (uint8_t)v;
+    o.op += 1;
+}
+
+// 255-run tail of a length field
+__device__ __forceinline__ void ring_len_ext(FastShared& F, FastOut& o, int lane, int64_t ext) {
+    const int64_t nff = ext / 255;
+    if (nff) ring_fill(F, o, lane, nff, 255);
+    ring_put(F, o, lane, (uint32_t)(ext - 255 * nff));
+}
+
+// src[pos, pos+n) -> output at op
+__device__ void ring_copy(FastShared& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n) {
+    if (n > kDirectLit) {
+        // head into the ring up to a 16-byte boundary, flush, bulk direct, tail into the ring
+        const int64_t h = (16 - (o.op & 15)) & 15;
+        ring_reserve(F, o, lane, 16);
+        if (lane < h) F.ring[(o.op + lane) & kRingMask] = (uint8_t)src_byte(j, pos + lane);
+        o.op += h; pos += h; n -= h;
+        ring_flush(F, o, lane);
+        const int64_t m = n & ~(int64_t)15;
+        const bool inb = (uint64_t)(pos + m) <= j.src_total;
+        for (int64_t t0 = 0; t0 < m; t0 += 16 * kWave * 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t t = t0 + 16 * (lane + kWave * u);
+                if (t < m) {
+                    if (inb) {
+                        __builtin_memcpy(&v[u], j.src + pos + t, 16);
+                    } else {
+                        uint32_t w[4];
+                        for (int q = 0; q < 4; ++q) w[q] = ld_u32(j, pos + t + 4 * q);
+                        v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t t = t0 + 16 * (lane + kWave * u);
+                if (t < m) __builtin_memcpy(o.dst + o.op + t, &v[u], 16);
+            }
+        }
+        o.op += m; pos += m; n -= m;
+        o.flushed = o.op;
+    }
+    ring_reserve(F, o, lane, n);
+    for (int64_t t = lane; t < n; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)src_byte(j, pos + t);
+    o.op += n;
+}
+
+// token + literal length + literals
+__device__ void fast_literals(FastShared& F, FastOut& o, const CompJob& j, int lane, int64_t anchor, int64_t lit,
+                              uint32_t mnib) {
+    ring_put(F, o, lane, (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib);
+    if (lit >= 15) ring_len_ext(F, o, lane, lit - 15);
+    if (lit) ring_copy(F, o, j, lane, anchor, lit);
+}
+
+__device__ __forceinline__ uint32_t code_of(const FastShared& F, uint32_t h) {
+    return (F.code[h >> 4] >> ((h & 15) * 2)) & 3u;
+}
+
+// entering epoch g: fields with code g mod 4 (stale, 4 epochs old) -> code (g+1) mod 4
+__device__ void scrub_epoch(FastShared& F, int lane, int32_t g) {
+    const uint32_t X = (uint32_t)(g & 3) * 0x55555555u, Y = (uint32_t)((g + 1) & 3) * 0x55555555u;
+    for (int w = lane; w < kCodeWords; w += kWave) {
+        const uint32_t v = F.code[w], x = v ^ X;
+        const uint32_t eq = ~(x | (x >> 1)) & 0x55555555u;
+        const uint32_t fm = eq | (eq << 1);
+        F.code[w] = (v & ~fm) | (Y & fm);
+    }
+}
+
+// First differing byte of src[a + t] vs src[b + t], t in [0, lim) (lim if none).
+__device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b, int64_t lim) {
+    int64_t base = 0;
+    while (base < lim) {
+        const uint32_t x = ld_u32(j, a + base + 4 * lane) ^ ld_u32(j, b + base + 4 * lane);
+        const uint64_t m = __ballot(x != 0);
+        if (m) {
+            const int fl = __builtin_ctzll(m);
+            const uint32_t xf = __shfl(x, fl, kWave);
+            const int64_t f = base + 4 * fl + (__builtin_ctz(xf) >> 3);
+            return f < lim ? f : lim;
+        }
+        base += 4 * kWave;
+    }
+    return lim;
+}
+
+__device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane) {
+    const int64_t n = j.len;
+    const int64_t mflimit = n - 12, matchlimit = n - 5;
+    FastOut o{j.dst, 0, 0};
+    int64_t i = 0, anchor = 0;
+    uint32_t c = 67;
+    int32_t g = 0;
+    for (int k = lane; k < 16384; k += kWave) F.lo[k] = 0;
+    for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
+    __syncthreads();
+    while (i < mflimit) {
+        while ((int32_t)(i >> 15) > g) scrub_epoch(F, lane, ++g);
+        // this batch's probe positions, assuming every probe misses
+        const uint32_t step = (c + lane) >> 6;
+        const uint32_t incl = wave_incl_scan(step, lane);
+        const int64_t p = i + (int64_t)(incl - step);
+        bool act = p < mflimit && (int32_t)(p >> 15) == g;
+        const uint32_t seq = act ? ld_u32(j, p) : 0u;
+        const uint32_t h = (seq * kP1) >> 18;
+        uint32_t lo = 0, cd = 0;
+        if (act) { lo = F.lo[h]; cd = code_of(F, h); }
+        // repeated hashes: one lane's id survives the write (volatile: the read-back
+        // must see other lanes' writes, not this lane's own value forwarded)
+        volatile uint16_t* vlo = F.lo;
+        if (act) vlo[h] = (uint16_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        const bool dup = act && vlo[h] != (uint16_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        if (act) vlo[h] = (uint16_t)lo;
+        int nb = __popcll(__ballot(act));                     // active lanes are a prefix
+        const uint64_t dm = __ballot(dup);
+        if (dm) { const int d = __builtin_ctzll(dm); nb = d ? d : 1; }
+        act = act && lane < nb;
+        int64_t cand = -1;
+        if (act && cd != (uint32_t)((g + 1) & 3)) {
+            const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
+            cand = ((int64_t)ge << 15) | (lo & 0x7FFFu);
+            if (ge < 0 || p - cand < 1 || p - cand > 65535) cand = -1;
+        }
+        const bool hit = cand >= 0 && ld_u32(j, cand) == seq;
+        const uint64_t hm = __ballot(hit);
+        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+        if (lane < nprobe) {                                  // the probes that happen insert their position
+            F.lo[h] = (uint16_t)(p & 0xFFFF);
+            const uint32_t sh = (h & 15) * 2;
+            atomicAnd(&F.code[h >> 4], ~(3u << sh));
+            atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
+        }
+        if (!hm) {
+            i = (int64_t)__shfl((int)(p + step), nb - 1, kWave);
+            c += nb;
+            continue;
+        }
+        const int m = nprobe - 1;
+        const int64_t pm = __shfl((int)p, m, kWave), cm = __shfl((int)cand, m, kWave);
+        c = 67;
+        const int64_t e = pm + 4 + match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
+        const int64_t mcode = e - pm - 4;
+        fast_literals(F, o, j, lane, anchor, pm - anchor, mcode >= 15 ? 15u : (uint32_t)mcode);
+        const uint32_t off = (uint32_t)(pm - cm);
+        ring_put(F, o, lane, off & 255);
+        ring_put(F, o, lane, (off >> 8) & 255);
+        if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
+        i = e;
+        anchor = e;
+    }
+    fast_literals(F, o, j, lane, anchor, n - anchor, 0);
+    ring_flush(F, o, lane);
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    return o.op;
+}
+
+__global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
+    __shared__ FastShared F;
+    const uint32_t b = blockIdx.x;
+    if (b >= a.nblocks) return;
+    CompJob j;
+    j.src = a.in + a.in_off[b];
+    j.src_total = a.in_len[b];
+    j.start = 0;
+    j.len = (int32_t)a.in_len[b];
+    j.dst = a.out + a.out_off[b];
+    j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
+    j.dst_pos = 0;
+    j.table = nullptr;
+    const int64_t r = compress_block_fast(j, F, threadIdx.x);
+    if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
+}
+
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
@@ -231,7 +485,7 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
     lz4mi::CompArgs a{};
     a.in = in; a.in_off = in_off; a.in_len = in_len; a.out = out; a.out_off = out_off; a.out_len = out_len;
     a.nblocks = nblocks;
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 
