@@ -15,7 +15,25 @@
 // module-global Int32Array(16384)).
 #include "lz4mi_common.h"
 
+#ifndef LZ4MI_CPROFILE
+#define LZ4MI_CPROFILE 0   // timing-only variant (tools/): per-phase wall-clock of the batch encoder
+#endif
+
 namespace lz4mi {
+
+#if LZ4MI_CPROFILE
+__device__ unsigned long long g_cprof[16];
+#define CPROF(i)                             \
+    do {                                     \
+        const uint64_t t_ = wall_clock64();  \
+        cprof[i] += t_ - cprof_t;            \
+        cprof_t = t_;                        \
+    } while (0)
+#define CPROF_COUNT(i, n) (cprof[i] += (n))
+#else
+#define CPROF(i) ((void)0)
+#define CPROF_COUNT(i, n) ((void)0)
+#endif
 
 struct CompJob {
     const uint8_t* src;   // positions are absolute from here
@@ -387,47 +405,127 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
     return lim;
 }
 
+// Sum over u < x of floor(u / 64): the miss-chain distance covered by the skip
+// steps (c + t) >> 6 is skip_sum(c + k) - skip_sum(c).
+__device__ __forceinline__ int64_t skip_sum(uint32_t x) {
+    const int64_t q = x >> 6, r = x & 63;
+    return 32 * q * (q - 1) + r * q;
+}
+
+// One sequence's bytes: token, literal length, literals, offset, match length.
+// Common case (at most 14 literals, match length field of at most one extra
+// byte) written by one ds_write_b8 per lane.
+__device__ __forceinline__ void emit_seq(FastShared& F, FastOut& o, const CompJob& j, int lane, int32_t anchor,
+                                         int32_t pm, uint32_t off, int32_t mcode) {
+    const int32_t lit = pm - anchor;
+    const uint32_t mnib = mcode >= 15 ? 15u : (uint32_t)mcode;
+    if (lit < 15 && mcode < 15 + 255) {
+        const int32_t total = 1 + lit + 2 + (mcode >= 15 ? 1 : 0);
+        ring_reserve(F, o, lane, total);
+        if (lane < total) {
+            uint32_t v;
+            if (lane == 0) v = ((uint32_t)lit << 4) | mnib;
+            else if (lane <= lit) v = src_byte(j, anchor + lane - 1);
+            else if (lane == lit + 1) v = off & 255;
+            else if (lane == lit + 2) v = (off >> 8) & 255;
+            else v = (uint32_t)(mcode - 15);
+            F.ring[(o.op + lane) & kRingMask] = (uint8_t)v;
+        }
+        o.op += total;
+        return;
+    }
+    fast_literals(F, o, j, lane, anchor, lit, mnib);
+    ring_put(F, o, lane, off & 255);
+    ring_put(F, o, lane, (off >> 8) & 255);
+    if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
+}
+
 __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane) {
-    const int64_t n = j.len;
-    const int64_t mflimit = n - 12, matchlimit = n - 5;
+    const int32_t n = j.len;
+    const int32_t mflimit = n - 12, matchlimit = n - 5;
     FastOut o{j.dst, 0, 0};
-    int64_t i = 0, anchor = 0;
+    int32_t i = 0, anchor = 0;
     uint32_t c = 67;
     int32_t g = 0;
+    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
+    uint32_t wl = 0;
+    // the previous match, emitted while the next probe's loads are in flight
+    bool pv = false;
+    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
+    uint32_t p_off = 0;
     for (int k = lane; k < 16384; k += kWave) F.lo[k] = 0;
     for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
     __syncthreads();
+#if LZ4MI_CPROFILE
+    uint64_t cprof[10] = {0};
+    uint64_t cprof_t = wall_clock64();
+#endif
     while (i < mflimit) {
-        while ((int32_t)(i >> 15) > g) scrub_epoch(F, lane, ++g);
+        CPROF(6);
+        CPROF_COUNT(8, 1);
+        while ((i >> 15) > g) scrub_epoch(F, lane, ++g);
         // this batch's probe positions, assuming every probe misses
+        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
         const uint32_t step = (c + lane) >> 6;
-        const uint32_t incl = wave_incl_scan(step, lane);
-        const int64_t p = i + (int64_t)(incl - step);
-        bool act = p < mflimit && (int32_t)(p >> 15) == g;
-        const uint32_t seq = act ? ld_u32(j, p) : 0u;
+        bool act = p < mflimit && (p >> 15) == g;
+        uint32_t seq = 0;
+        {   // from the window when it holds [p, p+4), else from memory
+            const int32_t off = p - wb;
+            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
+            const int wi = inw ? (off >> 2) : 0;
+            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
+            seq = funnel(w0, w1, (uint32_t)(off & 3));
+            if (__ballot(act && !inw)) {
+                if (act && !inw) seq = ld_u32(j, p);
+            }
+        }
         const uint32_t h = (seq * kP1) >> 18;
         uint32_t lo = 0, cd = 0;
         if (act) { lo = F.lo[h]; cd = code_of(F, h); }
-        // repeated hashes: one lane's id survives the write (volatile: the read-back
-        // must see other lanes' writes, not this lane's own value forwarded)
-        volatile uint16_t* vlo = F.lo;
-        if (act) vlo[h] = (uint16_t)lane;
-        __builtin_amdgcn_wave_barrier();
-        const bool dup = act && vlo[h] != (uint16_t)lane;
-        __builtin_amdgcn_wave_barrier();
-        if (act) vlo[h] = (uint16_t)lo;
+        CPROF(0);
         int nb = __popcll(__ballot(act));                     // active lanes are a prefix
-        const uint64_t dm = __ballot(dup);
-        if (dm) { const int d = __builtin_ctzll(dm); nb = d ? d : 1; }
-        act = act && lane < nb;
-        int64_t cand = -1;
+        int32_t cand = -1;
         if (act && cd != (uint32_t)((g + 1) & 3)) {
             const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
-            cand = ((int64_t)ge << 15) | (lo & 0x7FFFu);
+            cand = (ge << 15) | (int32_t)(lo & 0x7FFFu);
             if (ge < 0 || p - cand < 1 || p - cand > 65535) cand = -1;
         }
-        const bool hit = cand >= 0 && ld_u32(j, cand) == seq;
-        const uint64_t hm = __ballot(hit);
+        CPROF(1);
+        // verification loads, and (speculating that the first probe hits) the
+        // 256-byte extension windows of lane 0's candidate, in one round trip
+        const int32_t c0 = __shfl(cand, 0, kWave);
+        const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
+        uint32_t aw = 0, bw = 0;
+        if (c0 >= 0) {
+            aw = ld_u32(j, (int64_t)i + 4 + 4 * lane);
+            bw = ld_u32(j, (int64_t)c0 + 4 + 4 * lane);
+        }
+        if (pv) {                                             // overlaps the loads above
+            emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+            pv = false;
+        }
+        uint64_t hm = __ballot(cand >= 0 && vw == seq);
+        CPROF(2);
+        if (!(hm & 1ull) && nb > 1) {
+            // the first probe missed: a later lane's table read is only right if no
+            // earlier lane of the batch shares its hash (that probe would insert
+            // first). Write lane ids, read back: where ids collide, cut the batch
+            // before the first colliding lane. (volatile: the read-back must see
+            // other lanes' writes, not this lane's own value forwarded)
+            volatile uint16_t* vlo = F.lo;
+            if (act) vlo[h] = (uint16_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool dup = act && vlo[h] != (uint16_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            if (act) vlo[h] = (uint16_t)lo;
+            const uint64_t dm = __ballot(dup);
+            if (dm) {
+                const int d = __builtin_ctzll(dm);
+                nb = d ? d : 1;
+                hm &= (nb >= 64) ? ~0ull : ((1ull << nb) - 1);
+            }
+        }
+        CPROF(3);
         const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
         if (lane < nprobe) {                                  // the probes that happen insert their position
             F.lo[h] = (uint16_t)(p & 0xFFFF);
@@ -436,23 +534,50 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
             atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
         }
         if (!hm) {
-            i = (int64_t)__shfl((int)(p + step), nb - 1, kWave);
+            i = __shfl(p + (int32_t)step, nb - 1, kWave);
             c += nb;
             continue;
         }
+        CPROF(4);
+        CPROF_COUNT(9, 1);
         const int m = nprobe - 1;
-        const int64_t pm = __shfl((int)p, m, kWave), cm = __shfl((int)cand, m, kWave);
+        const int32_t pm = __shfl(p, m, kWave), cm = __shfl(cand, m, kWave);
         c = 67;
-        const int64_t e = pm + 4 + match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
-        const int64_t mcode = e - pm - 4;
-        fast_literals(F, o, j, lane, anchor, pm - anchor, mcode >= 15 ? 15u : (uint32_t)mcode);
-        const uint32_t off = (uint32_t)(pm - cm);
-        ring_put(F, o, lane, off & 255);
-        ring_put(F, o, lane, (off >> 8) & 255);
-        if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
+        const int32_t lim = matchlimit - (pm + 4);
+        int32_t f;
+        if (m == 0) {                     // extension from the speculative windows
+            const uint32_t x = aw ^ bw;
+            const uint64_t xm = __ballot(x != 0);
+            if (xm) {
+                const int fl = __builtin_ctzll(xm);
+                f = 4 * fl + (__builtin_ctz((uint32_t)__shfl(x, fl, kWave)) >> 3);
+            } else {
+                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, pm + 4 + 4 * kWave,
+                                                                        cm + 4 + 4 * kWave, lim - 4 * kWave)
+                                    : lim;
+            }
+            if (f > lim) f = lim;
+            wb = pm + 4;                  // the next probes' bytes come from this window
+            wl = aw;
+        } else {
+            f = (int32_t)match_extent(j, lane, pm + 4, cm + 4, lim);
+        }
+        const int32_t e = pm + 4 + f;
+        CPROF(5);
+        pv = true;
+        p_anchor = anchor;
+        p_pm = pm;
+        p_off = (uint32_t)(pm - cm);
+        p_mcode = e - pm - 4;
         i = e;
         anchor = e;
     }
+    if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+    CPROF(6);
+#if LZ4MI_CPROFILE
+    if (lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
+#endif
     fast_literals(F, o, j, lane, anchor, n - anchor, 0);
     ring_flush(F, o, lane);
     for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
@@ -477,6 +602,14 @@ __global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
 }
 
 }  // namespace lz4mi
+
+#if LZ4MI_CPROFILE
+extern "C" int lz4mi_debug_cprof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4mi::g_cprof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lz4mi::g_cprof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                             uint8_t* out, const uint64_t* out_off, uint32_t* out_len,

@@ -2,19 +2,22 @@
 # Build an alternative liblz4mi.so from the current sources with a sed edit
 # applied to the decoder (A/B timing with tools/microbench.py --so).
 #   tools/build_variant.sh NAME 'sed-expr' [extra hipcc flags]
+# FILE=lz4mi_compress.hip applies the edit to the encoder instead.
 set -e
 name=$1; expr=$2; shift 2
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/divortio-lz4_amd/csrc
 T=$(mktemp -d)
 cp $C/*.h $C/*.hip $C/*.cpp $T/
-sed -i "$expr" $T/lz4mi_decompress.hip
+F0=${FILE:-lz4mi_decompress.hip}
+sed -i "$expr" $T/$F0
 mkdir -p $R/tools/variants
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include $*"
 objs=""
-/opt/rocm/bin/hipcc $F -c -o $T/dec.o $T/lz4mi_decompress.hip & objs="$T/dec.o"
-for f in lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_capi.cpp; do
-  /opt/rocm/bin/hipcc $F -c -o $T/$f.o $C/$f & objs="$objs $T/$f.o"
+objs=""
+for f in lz4mi_decompress.hip lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_capi.cpp; do
+  if [ "$f" = "$F0" ]; then srcf=$T/$f; else srcf=$C/$f; fi
+  /opt/rocm/bin/hipcc $F -c -o $T/$f.o $srcf & objs="$objs $T/$f.o"
 done
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $R/tools/variants/liblz4mi_$name.so $objs
