@@ -13,12 +13,14 @@
 //  1. Stage it (+64 B lookahead) in LDS.
 //  2. next(p) of every position, branch-free (length fields of one extension
 //     byte; longer ones through a ballot-gated exact loop) into an LDS table.
-//  3. Speculative walks: lane l walks next() from 64 bytes before its 16-byte
+//  3. Speculative walks: lane l walks next() from 256 bytes before its 16-byte
 //     segment and records the tokens it visits in the segment; LZ4 token
 //     chains resynchronise within a few steps, so walks are almost always on
 //     the true chain. Certification left to right by ballot: the first lane
-//     whose left neighbour's exit is not on its walk re-walks from it. The
-//     result is the exact serial parse.
+//     whose left neighbour's exit is not on its walk re-walks from it (its
+//     neighbour is settled). The result is the exact serial parse. Walks
+//     start 256 bytes back: inside long literal runs a walk can take a while
+//     to fall onto the true chain, and every unsettled lane costs a pass.
 //  4. Sequence table in LDS (literal source, lengths, offset, output start by
 //     wave prefix sums) and errors in the reference's order.
 //  5. Output, sequence-parallel (lane l takes sequence 64i+l), every run
@@ -72,10 +74,11 @@ constexpr int kPad = 64;                      // lookahead for sequences straddl
 constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular sequence may touch
 constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
 constexpr int kMaxSeq = kChunk / 3 + 4;       // every non-final sequence is >= 3 bytes
+constexpr uint32_t kWarm = 256;               // speculative walks start this far before their segment
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
-constexpr int kB = 1;                         // pieces per lane per pipeline stage (lane-parallel runs)
+constexpr int kB = 4;                         // pieces per lane per pipeline stage (lane-parallel runs)
 constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 128;               // longer runs are written by the whole wave
@@ -455,17 +458,24 @@ struct WaveGen {
     }
 };
 
-// Pieces of each lane's own non-periodic match runs from earlier output:
-// sequences 64 i + lane for every bit i of `bits` (every piece a single window).
+// Each lane copies its own non-periodic match runs from earlier output
+// (sequences 64 i + lane for every bit i of `bits`), software-pipelined like
+// pipe() with a lean slot (every piece is one 16-byte window): y, source, width.
+struct LSlot {
+    int32_t y, a;
+    uint32_t w;   // 0 = none
+};
+
 struct LaneMatchGen {
     const Ctx& c;
     const DecShared& S;
     uint32_t bits;
     int lane, q, np;
     int32_t y, n, src;
-    __device__ __forceinline__ void fill(Slot (&s)[kB]) {
+    template <int NB>
+    __device__ __forceinline__ void fill(LSlot (&s)[NB]) {
 #pragma unroll
-        for (int j = 0; j < kB; ++j) {
+        for (int j = 0; j < NB; ++j) {
             while (q >= np && bits) {
                 const uint32_t k = 64u * __builtin_ctz(bits) + lane;
                 bits &= bits - 1;
@@ -486,14 +496,65 @@ struct LaneMatchGen {
                     w = n >= 8 ? 8u : 4u;             // match runs are >= 4 bytes
                     d = q ? n - (int32_t)w : 0;
                 }
-                s[j] = Slot{y + d, src + d, 16, 0, w | (1u << 8)};
+                s[j] = LSlot{y + d, src + d, w};
             } else {
-                s[j] = no_slot();
+                s[j] = LSlot{0, 0, 0u};
             }
             ++q;
         }
     }
 };
+
+template <int NB>
+__device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], uint4 (&A)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        if (s[j].w) {
+            const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(c.dst + s[j].a));
+            A[j] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        if (!s[j].w) continue;
+        if (LZ4MI_ABLATE == 4) {
+            if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pat[0] = 1;
+            continue;
+        }
+        if (s[j].w == 16) __builtin_memcpy(c.dst + s[j].y, &A[j], 16);
+        else store_w(c.dst + s[j].y, A[j], s[j].w);
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ bool any_lslot(const LSlot (&s)[NB]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) m |= s[j].w;
+    return m != 0;
+}
+
+template <int NB>
+__device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, LaneMatchGen& g) {
+    LSlot s0[NB], s1[NB];
+    uint4 a0[NB], a1[NB];
+    g.fill<NB>(s0);
+    lane_load<NB>(c, s0, a0);
+    for (;;) {
+        if (!__ballot(any_lslot<NB>(s0))) break;
+        g.fill<NB>(s1);
+        lane_load<NB>(c, s1, a1);
+        lane_store<NB>(c, S, s0, a0);
+        if (!__ballot(any_lslot<NB>(s1))) break;
+        g.fill<NB>(s0);
+        lane_load<NB>(c, s0, a0);
+        lane_store<NB>(c, S, s1, a1);
+    }
+}
 
 // A lane's match run the pipeline does not take (periodic, or byte-wise near a
 // buffer edge / in the dictionary): piece by piece.
@@ -702,11 +763,12 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         // ---- 3. speculative walks + certification -------------------------
         const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
         uint32_t vis = 0, x;
-        {   // 64-byte warm-up; lanes 0-3 start at the chunk start, a true token
-            uint32_t p = seg0 < 64 ? 0u : seg0 - 64;
+        {   // warm-up walk; lanes whose warm-up would start before the chunk start at it, a true token
+            uint32_t p = seg0 < kWarm ? 0u : seg0 - kWarm;
             while (p < seg1) {
                 if (p >= seg0) vis |= 1u << (p - seg0);
                 p = next_of(nxt, p);
+                PROF_COUNT(15, 1);
             }
             x = p;
         }
@@ -717,8 +779,10 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             nE = lane == 0 ? 0u : (pes >= seg0 ? pes : px);
             bool valid = nE >= seg1 ? (vis == 0 && x == nE) : ((vis >> (nE - seg0)) & 1u) != 0;
             uint64_t bad = __ballot(!valid);
+            PROF_COUNT(13, 1);
+            if (it == 0) PROF_COUNT(14, __popcll(bad));
             if (bad == 0) break;
-            if (lane == __builtin_ctzll(bad)) {     // first inconsistent lane: re-walk from its true entry
+            if (lane == __builtin_ctzll(bad)) {   // first inconsistent lane: re-walk from its true entry
                 vis = 0;
                 uint32_t p = nE;
                 while (p < seg1) {
@@ -843,7 +907,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         }
         {
             LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
-            pipe<R_HIST, false, kB>(c, S, g);
+            lane_pipe<kB>(c, S, g);
         }
         PROF(5);
         for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
@@ -893,7 +957,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             }
             {
                 LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
-                pipe<R_HIST, false, kB>(c, S, g);
+                lane_pipe<kB>(c, S, g);
             }
             __syncthreads();
         }

@@ -52,6 +52,8 @@ def main():
             print(f"{gen} blocks={n} kernel_ms={ms:.2f} wave_ms={tot:.2f} chunks/block={chunks:.0f} "
                   f"rounds/chunk={v[11] / n / max(1, chunks):.2f} cuts/block={v[12] / n:.1f} ok={ok}")
             print("   us/chunk:", per, flush=True)
+            print(f"   cert iterations/chunk={v[13] / n / max(1, chunks):.2f} initially-bad lanes/chunk="
+                  f"{v[14] / n / max(1, chunks):.2f} warm-up steps/lane/chunk={v[15] / n / max(1, chunks):.2f}")
             del raw, comp, dec
             torch.cuda.empty_cache()
 
