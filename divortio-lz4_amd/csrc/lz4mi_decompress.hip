@@ -595,7 +595,7 @@ __device__ __noinline__ void short_period_run(const Ctx& c, DecShared& S, int la
 }
 
 // The whole wave writes one run (uniform R).
-__device__ __noinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+__device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
     if (R.kind == R_NONE || R.n <= 0) return;
     if (R.kind == R_HIST && R.period && R.period < 16 && R.n > kShortPeriodBulk) {
         short_period_run(c, S, lane, R);
