@@ -558,7 +558,7 @@ __device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, LaneMatchG
 
 // A lane's match run the pipeline does not take (periodic, or byte-wise near a
 // buffer edge / in the dictionary): piece by piece.
-__device__ __noinline__ void lane_slow_run(const Ctx& c, const DecShared& S, const Run& R) {
+__device__ __forceinline__ void lane_slow_run(const Ctx& c, const DecShared& S, const Run& R) {
     const int np = run_pieces(R.n);
     for (int p = 0; p < np; ++p) {
         const Piece P = plan_piece(R, p);
@@ -636,7 +636,7 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
 
 // Wave-wide 255-run varint starting at block-relative q: returns the sum and
 // advances q past the terminating byte. Bytes past the block end read as 0.
-__device__ __noinline__ int64_t wave_varint(const Ctx& c, int lane, int64_t& q) {
+__device__ __forceinline__ int64_t wave_varint(const Ctx& c, int lane, int64_t& q) {
     int64_t sum = 0;
     for (;;) {
         int64_t p = q + 16 * lane;
