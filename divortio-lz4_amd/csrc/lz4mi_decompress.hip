@@ -342,7 +342,7 @@ __device__ __forceinline__ uint4 expand_period(uint4 A, int32_t r, int32_t per) 
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-__device__ __noinline__ void bytes_piece(const Ctx& c, int32_t y, int32_t a, int32_t src, uint32_t w, int32_t per) {
+__device__ __forceinline__ void bytes_piece(const Ctx& c, int32_t y, int32_t a, int32_t src, uint32_t w, int32_t per) {
     uint32_t o[4] = {0, 0, 0, 0};
     for (uint32_t j = 0; j < w; ++j) {
         const int32_t d = a + (int32_t)j;
@@ -576,7 +576,7 @@ __device__ __forceinline__ void lane_slow_run(const Ctx& c, const DecShared& S, 
 
 // Periodic run of period < 16 (long runs of a short pattern): the 16 bytes
 // at each phase are built once in LDS.
-__device__ __noinline__ void short_period_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+__device__ __forceinline__ void short_period_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
     const int32_t per = R.period;
     __syncthreads();
     for (int idx = lane; idx < 16 * per; idx += kWave) {
