@@ -89,6 +89,7 @@ struct DecShared {
     uint32_t t_out[kMaxSeq];      // output start of each sequence (block-relative)
     uint2 t_info[kMaxSeq];        // {literal source (chunk-relative) | literal length << 16,
                                   //  match offset | match length << 16 (0: final literal-only sequence)}
+    int32_t t_rsrc[kMaxSeq];      // round 1: a match's source mapped back to finished output (remap_src)
     union {
         uint16_t nxt[kLim];       // parse: next-token table
         uint32_t pme[kLim / 2];   // output: ends of the pending matches
@@ -458,6 +459,35 @@ struct WaveGen {
     }
 };
 
+// A match source [rs, re) inside this table's output, mapped back through the
+// sequences that wrote it (out[y] = out[y - off] inside a match): 1 = it now
+// lies in output finished by earlier chunks, 2 = in sequence j's literal run
+// (*lds = its stage index), 0 = it straddles sequences / the table start.
+__device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint32_t nseq, int32_t& rs, int32_t& re,
+                                         int32_t& lds) {
+    for (int d = 0; d < 8; ++d) {
+        if (re <= (int32_t)c.O) return 1;
+        if (rs < (int32_t)c.O) return 0;
+        uint32_t lo = 0, hi = nseq;                    // last sequence starting at or before rs
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((int32_t)S.t_out[mid] <= rs) lo = mid;
+            else hi = mid;
+        }
+        const int32_t t0 = (int32_t)S.t_out[lo];
+        const SeqInfo q = seq_info(S, lo);
+        const int32_t ms = t0 + q.ll;
+        if (re <= ms) {
+            lds = q.lit + (rs - t0);
+            return 2;
+        }
+        if (rs < ms || re > ms + q.ml) return 0;
+        rs -= q.off;
+        re -= q.off;
+    }
+    return 0;
+}
+
 // Each lane copies its own non-periodic match runs from earlier output
 // (sequences 64 i + lane for every bit i of `bits`), software-pipelined like
 // pipe() with a lean slot (every piece is one 16-byte window): y, source, width.
@@ -469,7 +499,7 @@ struct LSlot {
 struct LaneMatchGen {
     const Ctx& c;
     const DecShared& S;
-    uint32_t bits;
+    uint32_t bits, rbits;   // rbits: the source was remapped (S.t_rsrc)
     int lane, q, np;
     int32_t y, n, src;
     template <int NB>
@@ -477,13 +507,13 @@ struct LaneMatchGen {
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             while (q >= np && bits) {
-                const uint32_t k = 64u * __builtin_ctz(bits) + lane;
+                const uint32_t bi = __builtin_ctz(bits), k = 64u * bi + lane;
                 bits &= bits - 1;
                 const SeqInfo qi = seq_info(S, k);
                 const Run M = match_run(c, (int32_t)S.t_out[k] + qi.ll, qi.off, qi.ml);
                 y = M.y;
                 n = M.n;
-                src = M.src;
+                src = (rbits >> bi) & 1u ? S.t_rsrc[k] : M.src;
                 np = run_pieces(n);
                 q = 0;
             }
@@ -886,27 +916,49 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         // ---- 5. output rounds ---------------------------------------------
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         uint32_t ready = 0;   // bit i: ... is written by this lane in this round
+        uint32_t rbits = 0;   // bit i: ... reads a remapped source (S.t_rsrc)
         for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
             const uint32_t k = 64 * i + lane;
-            Run L = no_run(), M = no_run();
+            Run L = no_run(), M = no_run(), ML = no_run();
             if (k < nseq) {
                 const int32_t t0 = (int32_t)S.t_out[k];
                 const SeqInfo q = seq_info(S, k);
                 if (q.ll) L = Run{t0, q.ll, q.lit, 0, R_LDS};
                 M = match_run(c, t0 + q.ll, q.off, q.ml);
-                if (M.n == 0) M.kind = R_NONE;
-                else if (match_src_end(M) > (int32_t)c.O) { pend |= 1u << i; M.kind = R_NONE; }
+                if (M.n == 0) {
+                    M.kind = R_NONE;
+                } else if (match_src_end(M) > (int32_t)c.O) {
+                    // the source is output of this table: map it back through the
+                    // sequences that wrote it, else wait for a later round
+                    int32_t rs = M.src, re = match_src_end(M), li = 0;
+                    const int r = (M.kind == R_HIST && M.period == 0) ? remap_src(c, S, nseq, rs, re, li) : 0;
+                    if (r == 1) {
+                        M.src = rs;
+                        if (c.out_off + rs < 16) M.kind = R_BYTES;
+                        S.t_rsrc[k] = rs;
+                        rbits |= 1u << i;
+                    } else if (r == 2) {
+                        ML = Run{M.y, M.n, li, 0, R_LDS};
+                        M.kind = R_NONE;
+                    } else {
+                        pend |= 1u << i;
+                        M.kind = R_NONE;
+                    }
+                }
             }
             const bool longL = L.n > kLaneBytes, longM = M.kind != R_NONE && M.n > kLaneBytes;
+            const bool longML = ML.n > kLaneBytes;
             const bool fastM = M.kind == R_HIST && M.period == 0;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
             lane_literals(c, S, longL ? no_run() : L);
+            lane_literals(c, S, longML ? no_run() : ML);
+            for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)));
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
             for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
         }
         {
-            LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
+            LaneMatchGen g{c, S, ready, rbits, lane, 0, 0, 0, 0, 0};
             lane_pipe<kB>(c, S, g);
         }
         PROF(5);
@@ -956,7 +1008,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
             }
             {
-                LaneMatchGen g{c, S, ready, lane, 0, 0, 0, 0, 0};
+                LaneMatchGen g{c, S, ready, 0u, lane, 0, 0, 0, 0, 0};
                 lane_pipe<kB>(c, S, g);
             }
             __syncthreads();
