@@ -463,17 +463,15 @@ struct WaveGen {
 // sequences that wrote it (out[y] = out[y - off] inside a match): 1 = it now
 // lies in output finished by earlier chunks, 2 = in sequence j's literal run
 // (*lds = its stage index), 0 = it straddles sequences / the table start.
-__device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint32_t nseq, int32_t& rs, int32_t& re,
-                                         int32_t& lds) {
+// S.nxt doubles as an output -> sequence map during round 1: entry b is the
+// sequence holding output O + (b << sh) (built by the kernel before round 1).
+__device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint32_t nseq, uint32_t sh, int32_t& rs,
+                                         int32_t& re, int32_t& lds) {
     for (int d = 0; d < 8; ++d) {
         if (re <= (int32_t)c.O) return 1;
         if (rs < (int32_t)c.O) return 0;
-        uint32_t lo = 0, hi = nseq;                    // last sequence starting at or before rs
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((int32_t)S.t_out[mid] <= rs) lo = mid;
-            else hi = mid;
-        }
+        uint32_t lo = S.nxt[(uint32_t)(rs - (int32_t)c.O) >> sh];   // last sequence starting at or before rs
+        while (lo + 1 < nseq && (int32_t)S.t_out[lo + 1] <= rs) ++lo;
         const int32_t t0 = (int32_t)S.t_out[lo];
         const SeqInfo q = seq_info(S, lo);
         const int32_t ms = t0 + q.ll;
@@ -893,18 +891,47 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         int64_t cq = 0, cll = 0, cml = 0, clit = 0;
         uint32_t coff = 0;
         if (cut) {
-            int64_t q = (int64_t)c.ip + last_tok;
-            const uint32_t tok = q < c.in_len ? c.blk[q] : 0u;
-            ++q;
+            // token and literal length from the staged bytes while they last
+            constexpr uint32_t kStaged = 16 * (kStageWords / 4);
+            uint32_t r = last_tok;
+            const uint32_t tok = s[r++];
             cll = tok >> 4;
-            if (cll == 15) cll += wave_varint(c, lane, q);
+            bool more = cll == 15;
+            while (more && r < kStaged) {
+                const uint32_t b = s[r++];
+                cll += b;
+                more = b == 255;
+            }
+            int64_t q = (int64_t)c.ip + r;
+            if (more) cll += wave_varint(c, lane, q);
             clit = q;
             q += cll;
             if (q < c.in_len) {
-                coff = (uint32_t)c.blk[q] | ((uint32_t)(q + 1 < c.in_len ? c.blk[q + 1] : 0) << 8);
+                // offset and match length: one 16-byte load covers them unless the length runs on
+                uint32_t w[4];
+                if (q + 16 <= c.in_len) {
+                    __builtin_memcpy(w, c.blk + q, 16);
+                } else {
+                    for (int t = 0; t < 4; ++t) {
+                        uint32_t v = 0;
+                        for (int u = 0; u < 4; ++u)
+                            if (q + 4 * t + u < c.in_len) v |= (uint32_t)c.blk[q + 4 * t + u] << (8 * u);
+                        w[t] = v;
+                    }
+                }
+                coff = w[0] & 0xFFFFu;
                 q += 2;
                 cml = tok & 15;
-                if (cml == 15) cml += wave_varint(c, lane, q);
+                if (cml == 15) {
+                    bool run = true;
+                    for (int t = 2; t < 16 && run; ++t) {
+                        const uint32_t b = (w[t >> 2] >> (8 * (t & 3))) & 255u;
+                        cml += b;
+                        ++q;
+                        run = b == 255;
+                    }
+                    if (run) cml += wave_varint(c, lane, q);
+                }
                 cml += 4;
             }
             cq = q;
@@ -914,6 +941,15 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
         // ---- 5. output rounds ---------------------------------------------
+        // output -> sequence map for remap_src, in the (now idle) next-token table
+        uint32_t msh = 4;
+        while ((total >> msh) >= kLim) ++msh;
+        for (uint32_t k = lane; k < nseq; k += kWave) {
+            const uint32_t t0 = S.t_out[k] - (uint32_t)c.O;
+            const uint32_t t1 = (k + 1 < nseq ? S.t_out[k + 1] : (uint32_t)(c.O + total)) - (uint32_t)c.O;
+            for (uint32_t b = (t0 + (1u << msh) - 1) >> msh; (b << msh) < t1; ++b) S.nxt[b] = (uint16_t)k;
+        }
+        __syncthreads();
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         uint32_t ready = 0;   // bit i: ... is written by this lane in this round
         uint32_t rbits = 0;   // bit i: ... reads a remapped source (S.t_rsrc)
@@ -931,7 +967,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                     // the source is output of this table: map it back through the
                     // sequences that wrote it, else wait for a later round
                     int32_t rs = M.src, re = match_src_end(M), li = 0;
-                    const int r = (M.kind == R_HIST && M.period == 0) ? remap_src(c, S, nseq, rs, re, li) : 0;
+                    const int r = (M.kind == R_HIST && M.period == 0) ? remap_src(c, S, nseq, msh, rs, re, li) : 0;
                     if (r == 1) {
                         M.src = rs;
                         if (c.out_off + rs < 16) M.kind = R_BYTES;
