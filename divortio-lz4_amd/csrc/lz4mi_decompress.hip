@@ -500,36 +500,30 @@ struct LaneMatchGen {
     uint32_t bits, rbits;   // rbits: the source was remapped (S.t_rsrc)
     int lane, q, np;
     int32_t y, n, src;
+    // One batch = up to NB pieces of ONE run (runs are >= 16 bytes here, so
+    // every piece is a full 16-byte window; the last one overlaps its predecessor).
     template <int NB>
     __device__ __forceinline__ void fill(LSlot (&s)[NB]) {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            while (q >= np && bits) {
+        if (q >= np) {
+            np = 0;
+            q = 0;
+            if (bits) {
                 const uint32_t bi = __builtin_ctz(bits), k = 64u * bi + lane;
                 bits &= bits - 1;
                 const SeqInfo qi = seq_info(S, k);
-                const Run M = match_run(c, (int32_t)S.t_out[k] + qi.ll, qi.off, qi.ml);
-                y = M.y;
-                n = M.n;
-                src = (rbits >> bi) & 1u ? S.t_rsrc[k] : M.src;
-                np = run_pieces(n);
-                q = 0;
+                const int32_t ms = (int32_t)S.t_out[k] + qi.ll;
+                y = ms;
+                n = (ms + qi.ml > c.cap ? c.cap : ms + qi.ml) - ms;
+                src = (rbits >> bi) & 1u ? S.t_rsrc[k] : ms - qi.off;
+                np = (n + 15) >> 4;
             }
-            if (q < np) {
-                uint32_t w = 16;
-                int32_t d;
-                if (n >= 16) {
-                    d = 16 * q < n - 16 ? 16 * q : n - 16;
-                } else {
-                    w = n >= 8 ? 8u : 4u;             // match runs are >= 4 bytes
-                    d = q ? n - (int32_t)w : 0;
-                }
-                s[j] = LSlot{y + d, src + d, w};
-            } else {
-                s[j] = LSlot{0, 0, 0u};
-            }
-            ++q;
         }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int32_t d = 16 * (q + j) < n - 16 ? 16 * (q + j) : n - 16;
+            s[j] = LSlot{y + d, src + d, q + j < np ? 16u : 0u};
+        }
+        q += NB;
     }
 };
 
@@ -553,8 +547,7 @@ __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSl
             if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pat[0] = 1;
             continue;
         }
-        if (s[j].w == 16) __builtin_memcpy(c.dst + s[j].y, &A[j], 16);
-        else store_w(c.dst + s[j].y, A[j], s[j].w);
+        __builtin_memcpy(c.dst + s[j].y, &A[j], 16);
     }
 }
 
@@ -650,15 +643,28 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
 
 // Each lane copies its own short literal runs (LDS -> output; no vector-memory loads).
 __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L) {
-    const int np = L.kind == R_NONE ? 0 : run_pieces(L.n);
-    for (int q = 0; __ballot(q < np) != 0; q += 2) {
-        const Piece P0 = plan_piece(L, q < np ? q : np), P1 = plan_piece(L, q + 1 < np ? q + 1 : np);
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
-        if (P0.mode) __builtin_memcpy(&v0, (const uint8_t*)S.stage + P0.a, 16);
-        if (P1.mode) __builtin_memcpy(&v1, (const uint8_t*)S.stage + P1.a, 16);
+    const int32_t n = L.kind == R_NONE ? 0 : L.n;
+    const int np = n >= 16 ? (n + 15) >> 4 : 0;
+    for (int q = 0; __ballot(q < np) != 0; q += 2) {       // runs of >= 16 bytes: 16-byte pieces
+        const int32_t d0 = 16 * q < n - 16 ? 16 * q : n - 16, d1 = 16 * (q + 1) < n - 16 ? 16 * (q + 1) : n - 16;
+        uint4 v0, v1;
+        __builtin_memcpy(&v0, (const uint8_t*)S.stage + L.src + d0, 16);
+        __builtin_memcpy(&v1, (const uint8_t*)S.stage + L.src + d1, 16);
         if (LZ4MI_ABLATE == 4) continue;
-        if (P0.mode) store_w(c.dst + P0.y, v0, P0.w);
-        if (P1.mode) store_w(c.dst + P1.y, v1, P1.w);
+        if (q < np) __builtin_memcpy(c.dst + L.y + d0, &v0, 16);
+        if (q + 1 < np) __builtin_memcpy(c.dst + L.y + d1, &v1, 16);
+    }
+    if (__ballot(n > 0 && n < 16)) {                       // shorter runs: two overlapping 8/4/2/1-byte stores
+        if (n > 0 && n < 16) {
+            const uint32_t w = n >= 8 ? 8u : n >= 4 ? 4u : n >= 2 ? 2u : 1u;
+            uint4 v0, v1;
+            __builtin_memcpy(&v0, (const uint8_t*)S.stage + L.src, 16);
+            __builtin_memcpy(&v1, (const uint8_t*)S.stage + L.src + n - (int32_t)w, 16);
+            if (LZ4MI_ABLATE != 4) {
+                store_w(c.dst + L.y, v0, w);
+                store_w(c.dst + L.y + n - (int32_t)w, v1, w);
+            }
+        }
     }
 }
 
@@ -984,7 +990,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             }
             const bool longL = L.n > kLaneBytes, longM = M.kind != R_NONE && M.n > kLaneBytes;
             const bool longML = ML.n > kLaneBytes;
-            const bool fastM = M.kind == R_HIST && M.period == 0;
+            const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
             lane_literals(c, S, longL ? no_run() : L);
             lane_literals(c, S, longML ? no_run() : ML);
@@ -1038,7 +1044,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                     else M.kind = R_NONE;
                 }
                 const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
-                const bool fastM = M.kind == R_HIST && M.period == 0;
+                const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
                 if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
                 if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
