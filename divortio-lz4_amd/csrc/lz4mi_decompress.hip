@@ -56,7 +56,7 @@
 namespace lz4mi {
 
 #if LZ4MI_PROFILE
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[24];
 #define PROF(i)                              \
     do {                                     \
         const uint64_t t_ = wall_clock64();  \
@@ -113,6 +113,20 @@ struct Ctx {
     int32_t ip;           // chunk start (block-relative compressed position)
     int64_t O;            // output start of the current table (block-relative)
 };
+
+// 16 compressed bytes at block-relative r0 (zero past the block end).
+__device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + 16 <= c.in_len) {
+        __builtin_memcpy(&v, c.blk + r0, 16);
+    } else if (r0 < c.in_len) {
+        uint32_t o[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; ++j)
+            if (r0 + j < c.in_len) o[j >> 2] |= (uint32_t)c.blk[r0 + j] << (8 * (j & 3));
+        v = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    return v;
+}
 
 // ---------------------------------------------------------------- parsing
 // Position of the token after the one at p (chunk-relative), or kEnd / kStop.
@@ -747,30 +761,24 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
+    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
+    bool have_pf = false;
 #if LZ4MI_PROFILE
-    uint64_t prof[16] = {0};
+    uint64_t prof[24] = {0};
     uint64_t prof_t = wall_clock64();
 #endif
 
     while (c.ip < c.in_len) {
         PROF_COUNT(10, 1);
-        // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads) ------------
-        {
-            uint8_t* st = (uint8_t*)S.stage;
-            for (int k = lane; k < kStageWords / 4; k += kWave) {
-                const int64_t r0 = (int64_t)c.ip + 16 * k;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (r0 + 16 <= c.in_len) {
-                    __builtin_memcpy(&v, c.blk + r0, 16);
-                } else {
-                    uint32_t o[4] = {0, 0, 0, 0};
-                    for (int j = 0; j < 16; ++j)
-                        if (r0 + j < c.in_len) o[j >> 2] |= (uint32_t)c.blk[r0 + j] << (8 * (j & 3));
-                    v = make_uint4(o[0], o[1], o[2], o[3]);
-                }
-                __builtin_memcpy(st + 16 * k, &v, 16);
-            }
+        // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
+        // the previous chunk's output phase, ahead of its stores) -------------
+        if (!have_pf) {
+            pf0 = stage_piece(c, (int64_t)c.ip + 16 * lane);
+            if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, (int64_t)c.ip + 16 * (kWave + lane));
         }
+        have_pf = false;
+        __builtin_memcpy((uint8_t*)S.stage + 16 * lane, &pf0, 16);
+        if (lane < kStageWords / 4 - kWave) __builtin_memcpy((uint8_t*)S.stage + 16 * (kWave + lane), &pf1, 16);
         __syncthreads();
         const uint8_t* s = (const uint8_t*)S.stage;
         const uint32_t rem = (uint32_t)(c.in_len - c.ip);
@@ -931,7 +939,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                 if (cml == 15) {
                     bool run = true;
                     for (int t = 2; t < 16 && run; ++t) {
-                        const uint32_t b = (w[t >> 2] >> (8 * (t & 3))) & 255u;
+                        const uint32_t wd = t < 4 ? w[0] : t < 8 ? w[1] : t < 12 ? w[2] : w[3];
+                        const uint32_t b = (wd >> (8 * (t & 3))) & 255u;
                         cml += b;
                         ++q;
                         run = b == 255;
@@ -943,6 +952,15 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             cq = q;
         }
         const int64_t tab_hi = c.O + total;
+        {   // the next chunk's bytes: their loads go out before this chunk's stores
+            const int64_t nip = cut ? (cq < c.in_len ? cq : c.in_len)
+                                    : (tail >= kEnd ? (int64_t)c.in_len : (int64_t)c.ip + tail);
+            if (nip < c.in_len) {
+                pf0 = stage_piece(c, nip + 16 * lane);
+                if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+                have_pf = true;
+            }
+        }
 
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
@@ -992,18 +1010,21 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             const bool longML = ML.n > kLaneBytes;
             const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
+            PROF(16);
             lane_literals(c, S, longL ? no_run() : L);
             lane_literals(c, S, longML ? no_run() : ML);
+            PROF(17);
             for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)));
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
             for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+            PROF(18);
         }
         {
             LaneMatchGen g{c, S, ready, rbits, lane, 0, 0, 0, 0, 0};
             lane_pipe<kB>(c, S, g);
         }
-        PROF(5);
+        PROF(19);
         for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
             uint32_t np = 0;
             for (uint32_t i = 0; 64 * i < nseq; ++i) {
@@ -1024,6 +1045,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             PROF_COUNT(11, 1);
             __syncthreads();
             wait_vmem();      // the previous round's stores are complete
+            PROF(20);
             ready = 0;
             for (uint32_t i = 0; 64 * i < nseq; ++i) {
                 if (__ballot((pend >> i) & 1u) == 0) continue;
@@ -1099,7 +1121,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     }
 #if LZ4MI_PROFILE
     if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
+        for (int i = 0; i < 24; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
 #endif
     if (lane == 0) {
         a.status[b] = status;
@@ -1112,8 +1134,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 #if LZ4MI_PROFILE
 // Per-phase wall-clock ticks (100 MHz) summed over all waves since the last call; resets.
 extern "C" int lz4mi_debug_prof(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4mi::g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    unsigned long long z[16] = {0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4mi::g_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
+    unsigned long long z[24] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(lz4mi::g_prof), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif

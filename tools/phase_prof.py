@@ -21,7 +21,7 @@ def main():
     L.lz4mi_decompress_blocks.restype = ctypes.c_int32
     assert L.lz4mi_init(0) == 0
     s = torch.cuda.Stream(); torch.cuda.set_stream(s); sp = s.cuda_stream
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 24)()
     for gen in a.gens.split(","):
         for n in map(int, a.blocks.split(",")):
             raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
@@ -52,6 +52,9 @@ def main():
             print(f"{gen} blocks={n} kernel_ms={ms:.2f} wave_ms={tot:.2f} chunks/block={chunks:.0f} "
                   f"rounds/chunk={v[11] / n / max(1, chunks):.2f} cuts/block={v[12] / n:.1f} ok={ok}")
             print("   us/chunk:", per, flush=True)
+            extra = {nm: round(v[i] / 100.0 / n / max(1, chunks), 3) for i, nm in
+                     ((16, "r1_groupsetup"), (17, "r1_literals"), (18, "r1_slow+long"), (19, "r1_pipe"), (20, "rN_compact+wait"))}
+            print("   round-1 split:", extra)
             print(f"   cert iterations/chunk={v[13] / n / max(1, chunks):.2f} initially-bad lanes/chunk="
                   f"{v[14] / n / max(1, chunks):.2f} warm-up steps/lane/chunk={v[15] / n / max(1, chunks):.2f}")
             del raw, comp, dec
