@@ -17,7 +17,7 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, c
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
                                               int32_t*, uint32_t, int, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
-                                            const uint64_t*, uint32_t*, uint32_t, hipStream_t);
+                                            const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int32_t, int32_t, int32_t*, uint8_t*,
                                                   uint64_t, int32_t, int64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
@@ -46,6 +46,7 @@ struct Ctx {
     int device = -1;
     hipStream_t stream = nullptr;
     Scratch in, out, meta, aux;
+    Scratch tables;   // batch encoder hash tables (64 KiB per block)
     std::mutex mu;
 };
 
@@ -239,7 +240,12 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
     if (st) return st;
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
-        LZ4MI_TRY(lz4mi_launch_compress(in, in_off, in_len, out, out_off, out_len, nblocks, pick_stream(stream)));
+        // the table scratch is the context's: launches through it are serialised on the context's lock
+        // and ordered on one stream per context use (see include/lz4mi.h)
+        std::lock_guard<std::mutex> lk(g_ctx.mu);
+        LZ4MI_TRY(g_ctx.tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t)));
+        LZ4MI_TRY(lz4mi_launch_compress(in, in_off, in_len, out, out_off, out_len, nblocks, g_ctx.tables.as<int32_t>(),
+                                        pick_stream(stream)));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_len) return LZ4MI_ERR_ARG;
@@ -266,8 +272,9 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
     LZ4MI_TRY(hipMemcpyAsync(m_in_off, d_in_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
+    LZ4MI_TRY(g_ctx.tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t)));
     LZ4MI_TRY(lz4mi_launch_compress(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off,
-                                    m_out_len, nblocks, s));
+                                    m_out_len, nblocks, g_ctx.tables.as<int32_t>(), s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
     for (uint32_t b = 0; b < nblocks; ++b)

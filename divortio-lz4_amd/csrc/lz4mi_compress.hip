@@ -15,6 +15,8 @@
 // module-global Int32Array(16384)).
 #include "lz4mi_common.h"
 
+#include <cstdlib>
+
 #ifndef LZ4MI_CPROFILE
 #define LZ4MI_CPROFILE 0   // timing-only variant (tools/): per-phase wall-clock of the batch encoder
 #endif
@@ -287,7 +289,8 @@ __device__ __forceinline__ uint32_t ld_u32(const CompJob& j, int64_t p) {
 }
 
 // ring [flushed, floor16(op)) -> dst
-__device__ void ring_flush(FastShared& F, FastOut& o, int lane) {
+template <class SH>
+__device__ void ring_flush(SH& F, FastOut& o, int lane) {
     const int64_t upto = o.op & ~(int64_t)15;
     for (int64_t p = o.flushed + 16 * lane; p < upto; p += 16 * kWave) {
         uint4 v;
@@ -297,12 +300,14 @@ __device__ void ring_flush(FastShared& F, FastOut& o, int lane) {
     if (upto > o.flushed) o.flushed = upto;
 }
 
-__device__ __forceinline__ void ring_reserve(FastShared& F, FastOut& o, int lane, int64_t n) {
+template <class SH>
+__device__ __forceinline__ void ring_reserve(SH& F, FastOut& o, int lane, int64_t n) {
     if (o.op + n - o.flushed > kRing) ring_flush(F, o, lane);
 }
 
 // n bytes of value v (n <= kRing - 16 per call)
-__device__ void ring_fill(FastShared& F, FastOut& o, int lane, int64_t n, uint32_t v) {
+template <class SH>
+__device__ void ring_fill(SH& F, FastOut& o, int lane, int64_t n, uint32_t v) {
     while (n > 0) {
         const int64_t k = n < kRing - 16 ? n : kRing - 16;
         ring_reserve(F, o, lane, k);
@@ -312,21 +317,24 @@ __device__ void ring_fill(FastShared& F, FastOut& o, int lane, int64_t n, uint32
     }
 }
 
-__device__ __forceinline__ void ring_put(FastShared& F, FastOut& o, int lane, uint32_t v) {
+template <class SH>
+__device__ __forceinline__ void ring_put(SH& F, FastOut& o, int lane, uint32_t v) {
     ring_reserve(F, o, lane, 1);
     if (lane == 0) F.ring[o.op & kRingMask] = (uint8_t)v;
     o.op += 1;
 }
 
 // 255-run tail of a length field
-__device__ __forceinline__ void ring_len_ext(FastShared& F, FastOut& o, int lane, int64_t ext) {
+template <class SH>
+__device__ __forceinline__ void ring_len_ext(SH& F, FastOut& o, int lane, int64_t ext) {
     const int64_t nff = ext / 255;
     if (nff) ring_fill(F, o, lane, nff, 255);
     ring_put(F, o, lane, (uint32_t)(ext - 255 * nff));
 }
 
 // src[pos, pos+n) -> output at op
-__device__ void ring_copy(FastShared& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n) {
+template <class SH>
+__device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n) {
     if (n > kDirectLit) {
         // head into the ring up to a 16-byte boundary, flush, bulk direct, tail into the ring
         const int64_t h = (16 - (o.op & 15)) & 15;
@@ -366,7 +374,8 @@ __device__ void ring_copy(FastShared& F, FastOut& o, const CompJob& j, int lane,
 }
 
 // token + literal length + literals
-__device__ void fast_literals(FastShared& F, FastOut& o, const CompJob& j, int lane, int64_t anchor, int64_t lit,
+template <class SH>
+__device__ void fast_literals(SH& F, FastOut& o, const CompJob& j, int lane, int64_t anchor, int64_t lit,
                               uint32_t mnib) {
     ring_put(F, o, lane, (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib);
     if (lit >= 15) ring_len_ext(F, o, lane, lit - 15);
@@ -415,7 +424,8 @@ __device__ __forceinline__ int64_t skip_sum(uint32_t x) {
 // One sequence's bytes: token, literal length, literals, offset, match length.
 // Common case (at most 14 literals, match length field of at most one extra
 // byte) written by one ds_write_b8 per lane.
-__device__ __forceinline__ void emit_seq(FastShared& F, FastOut& o, const CompJob& j, int lane, int32_t anchor,
+template <class SH>
+__device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, int lane, int32_t anchor,
                                          int32_t pm, uint32_t off, int32_t mcode) {
     const int32_t lit = pm - anchor;
     const uint32_t mnib = mcode >= 15 ? 15u : (uint32_t)mcode;
@@ -601,6 +611,178 @@ __global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
+// ---------------------------------------------------------------------------
+// Batch encoder with the hash tables in global memory: one Int32Array(16384)
+// per block (values = position + 1, as the reference's), so LDS only holds the
+// output ring and 16 blocks run per CU instead of 4. A probe at the chain's
+// head reads and replaces its table slot with one atomic exchange (the
+// reference's insert-before-verify in a single operation); after a miss the
+// following probes go as a 64-wide batch like compress_block_fast's (table read
+// with plain L1-bypassing loads, the probes that happen store their positions,
+// and the stores complete before the next table access).
+struct GtShared {
+    uint8_t ring[kRing];
+    uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
+};
+
+__device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, int lane) {
+    const int32_t n = j.len;
+    const int32_t mflimit = n - 12, matchlimit = n - 5;
+    FastOut o{j.dst, 0, 0};
+    int32_t i = 0, anchor = 0;
+    uint32_t c = 67;
+    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
+    uint32_t wl = 0;
+    bool pv = false;             // the previous match, emitted while the next probe's loads are in flight
+    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
+    uint32_t p_off = 0;
+    for (int k = lane; k < 16384 / 4; k += kWave) ((uint4*)T)[k] = make_uint4(0, 0, 0, 0);
+    wait_vmem();                 // the table is zero before the first exchange
+    while (i < mflimit) {
+        // ---- the probe at i: one exchange, then verification + speculative extension windows
+        const int32_t off0 = i - wb;
+        uint32_t seq0;
+        if (off0 >= 0 && off0 + 4 <= 4 * kWave) {
+            const int wi = off0 >> 2;
+            seq0 = funnel(__builtin_amdgcn_readlane(wl, wi), __builtin_amdgcn_readlane(wl, wi < kWave - 1 ? wi + 1 : wi),
+                          (uint32_t)(off0 & 3));
+        } else {
+            seq0 = uniform(ld_u32(j, i));
+        }
+        const uint32_t h0 = (seq0 * kP1) >> 18;
+        int32_t old = 0;
+        if (lane == 0) old = atomicExch(&T[h0], i + 1);
+        old = (int32_t)uniform((uint32_t)old);
+        int32_t cand0 = old - 1;
+        if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
+        uint32_t aw = 0, bw = 0;
+        bool hit0 = false;
+        if (cand0 >= 0) {
+            const uint32_t vw = ld_u32(j, cand0);
+            aw = ld_u32(j, (int64_t)i + 4 + 4 * lane);
+            bw = ld_u32(j, (int64_t)cand0 + 4 + 4 * lane);
+            if (pv) {
+                emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+                pv = false;
+            }
+            hit0 = uniform(vw) == seq0;
+        }
+        if (hit0) {
+            c = 67;
+            const int32_t lim = matchlimit - (i + 4);
+            const uint32_t x = aw ^ bw;
+            const uint64_t xm = __ballot(x != 0);
+            int32_t f;
+            if (xm) {
+                const int fl = __builtin_ctzll(xm);
+                f = 4 * fl + (__builtin_ctz((uint32_t)__shfl(x, fl, kWave)) >> 3);
+            } else {
+                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, i + 4 + 4 * kWave,
+                                                                        cand0 + 4 + 4 * kWave, lim - 4 * kWave)
+                                    : lim;
+            }
+            if (f > lim) f = lim;
+            wb = i + 4;
+            wl = aw;
+            const int32_t e = i + 4 + f;
+            pv = true;
+            p_anchor = anchor;
+            p_pm = i;
+            p_off = (uint32_t)(i - cand0);
+            p_mcode = e - i - 4;
+            i = e;
+            anchor = e;
+            continue;
+        }
+        if (pv) {
+            emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+            pv = false;
+        }
+        // ---- the probe at i missed (and inserted itself): the next probes of the miss chain as a batch
+        i += (int32_t)(c >> 6);
+        c += 1;
+        if (i >= mflimit) break;
+        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const uint32_t step = (c + lane) >> 6;
+        bool act = p < mflimit;
+        uint32_t seq = 0;
+        {
+            const int32_t off = p - wb;
+            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
+            const int wi = inw ? (off >> 2) : 0;
+            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
+            seq = funnel(w0, w1, (uint32_t)(off & 3));
+            if (__ballot(act && !inw)) {
+                if (act && !inw) seq = ld_u32(j, p);
+            }
+        }
+        const uint32_t h = (seq * kP1) >> 18;
+        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
+            volatile uint8_t* vs = F.slot;
+            if (act) vs[h & 1023] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool dup = act && vs[h & 1023] != (uint8_t)lane;
+            int nb = __popcll(__ballot(act));
+            const uint64_t dm = __ballot(dup);
+            if (dm) {
+                const int d = __builtin_ctzll(dm);
+                nb = d ? d : 1;
+            }
+            act = act && lane < nb;
+        }
+        const int nb = __popcll(__ballot(act));
+        int32_t cand = -1;
+        if (act) {
+            const int32_t ov = __builtin_nontemporal_load(&T[h]);
+            cand = ov - 1;
+            if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
+        }
+        const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
+        const uint64_t hm = __ballot(cand >= 0 && vw == seq);
+        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+        if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
+        wait_vmem();                                           // ... before the next table access
+        if (!hm) {
+            i = __shfl(p + (int32_t)step, nb - 1, kWave);
+            c += nb;
+            continue;
+        }
+        const int m = nprobe - 1;
+        const int32_t pm = __shfl(p, m, kWave), cm = __shfl(cand, m, kWave);
+        c = 67;
+        const int32_t e = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
+        pv = true;
+        p_anchor = anchor;
+        p_pm = pm;
+        p_off = (uint32_t)(pm - cm);
+        p_mcode = e - pm - 4;
+        i = e;
+        anchor = e;
+    }
+    if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+    fast_literals(F, o, j, lane, anchor, n - anchor, 0);
+    ring_flush(F, o, lane);
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    return o.op;
+}
+
+__global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, int32_t* tables) {
+    __shared__ GtShared F;
+    const uint32_t b = blockIdx.x;
+    if (b >= a.nblocks) return;
+    CompJob j;
+    j.src = a.in + a.in_off[b];
+    j.src_total = a.in_len[b];
+    j.start = 0;
+    j.len = (int32_t)a.in_len[b];
+    j.dst = a.out + a.out_off[b];
+    j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
+    j.dst_pos = 0;
+    j.table = nullptr;
+    const int64_t r = compress_block_gt(j, F, tables + (size_t)b * 16384, threadIdx.x);
+    if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
+}
+
 }  // namespace lz4mi
 
 #if LZ4MI_CPROFILE
@@ -613,12 +795,19 @@ extern "C" int lz4mi_debug_cprof(unsigned long long* out) {
 
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                             uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
-                                            uint32_t nblocks, hipStream_t stream) {
+                                            uint32_t nblocks, int32_t* tables, hipStream_t stream) {
     if (nblocks == 0) return hipSuccess;
     lz4mi::CompArgs a{};
     a.in = in; a.in_off = in_off; a.in_len = in_len; a.out = out; a.out_off = out_off; a.out_len = out_len;
     a.nblocks = nblocks;
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    // encoder: LZ4MI_ENCODER=lds selects the LDS-table kernel (4 blocks per CU);
+    // default: global tables (16 blocks per CU; `tables` = 64 KiB per block of scratch)
+    static const char* enc = getenv("LZ4MI_ENCODER");
+    if (enc && enc[0] == 'l') {
+        hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
     return hipGetLastError();
 }
 
