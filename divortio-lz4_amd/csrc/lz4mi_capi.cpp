@@ -18,6 +18,9 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, c
                                               int32_t*, uint32_t, int, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
+extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
+                                              const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*, uint32_t,
+                                              hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int32_t, int32_t, int32_t*, uint8_t*,
                                                   uint64_t, int32_t, int64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
@@ -349,6 +352,17 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
     LZ4MI_TRY(lz4mi_launch_xxh32(g_ctx.in.as<uint8_t>(), m_off, m_len, seed, m_h, nblocks, stdv, s));
     LZ4MI_TRY(hipMemcpyAsync(hashes, m_h, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
+    return LZ4MI_OK;
+}
+
+int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len, const uint8_t* comp,
+                         const uint64_t* comp_off, const uint32_t* comp_len, uint8_t* frame, const uint64_t* rec_off,
+                         uint32_t nblocks, uint32_t flags, void* stream) {
+    int32_t st = ensure_init();
+    if (st) return st;
+    if (!(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
+    LZ4MI_TRY(lz4mi_launch_frame_pack(raw, raw_off, raw_len, comp, comp_off, comp_len, frame, rec_off, nblocks,
+                                      pick_stream(stream)));
     return LZ4MI_OK;
 }
 

@@ -33,7 +33,7 @@ GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GE
 # every symbol include/lz4mi.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_version",
            "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
-           "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_generate_blocks")
+           "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks")
 
 
 class Lz4miError(RuntimeError):
@@ -77,6 +77,8 @@ def lib():
         L.lz4mi_xxh32.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32]
         L.lz4mi_xxh32_blocks.restype = ctypes.c_int32
         L.lz4mi_xxh32_blocks.argtypes = [_vp, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
+        L.lz4mi_frame_pack.restype = ctypes.c_int32
+        L.lz4mi_frame_pack.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
         L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, _vp]
@@ -251,3 +253,10 @@ def xxh32_blocks_dev(in_ptr, off_ptr, len_ptr, hashes_ptr, nblocks, seed=0, stre
 def generate_blocks_dev(out_ptr, kind, seed0, block_size, nblocks, stream=0):
     k = GENERATORS[kind] if isinstance(kind, str) else kind
     _check(lib().lz4mi_generate_blocks(out_ptr, k, seed0, block_size, nblocks, stream or None))
+
+
+def frame_pack_dev(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr, rec_off_ptr,
+                   nblocks, stream=0):
+    """Device-side frame block records (size word + compressed or stored payload) at rec_off."""
+    _check(lib().lz4mi_frame_pack(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr,
+                                  rec_off_ptr, nblocks, DEVICE_PTRS, stream or None))

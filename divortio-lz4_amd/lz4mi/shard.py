@@ -13,6 +13,10 @@ gloo on CPU):
 Each rank's records are already laid out exactly as the reference's block loop
 writes them (bufferCompress.js:209-239): LE32 size + payload when
 0 < compSize < blockSize, else LE32 (blockSize | 0x80000000) + the raw block.
+`gather_records_to_root` is the device-resident variant used when one rank
+writes the frame: records packed on each GPU by `lz4mi_frame_pack`, byte counts
+all-gathered, then exactly those bytes sent point-to-point to the root (no
+padding, no copy to every rank).
 `frame_blocks` is the inverse walk for decoding (bufferDecompress.js:133-192).
 """
 import numpy as np
@@ -64,6 +68,48 @@ def gather_frame(local_records, header, trailer, group=None, device="cpu"):
     end = np.zeros(4, dtype=np.uint8)
     return np.concatenate([np.frombuffer(bytes(header), dtype=np.uint8)] + body +
                           [end, np.frombuffer(bytes(trailer), dtype=np.uint8)])
+
+
+def record_sizes(comp_len, raw_len):
+    """Per-block frame record sizes (torch int64): 4 + payload (compressed when 0 < comp < raw)."""
+    import torch
+    comp = comp_len.to(torch.int64)
+    raw = raw_len.to(torch.int64)
+    return 4 + torch.where((comp > 0) & (comp < raw), comp, raw)
+
+
+def gather_records_to_root(records, root=0, group=None):
+    """Concatenate every rank's record bytes (1-D uint8 tensor, any device the
+    backend supports) on `root`, in rank order: an all-gather of the byte
+    counts, then point-to-point sends of exactly those bytes (RCCL over xGMI with
+    the nccl backend). Returns the concatenation on root, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = records.device
+    n = torch.tensor([records.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    if rank != root:
+        if sizes[rank]:
+            dist.send(records, dst=root, group=group)
+        return None
+    out = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+    offs = [0]
+    for x in sizes:
+        offs.append(offs[-1] + x)
+    reqs = []
+    for r in range(world):
+        if r == root:
+            out[offs[r]:offs[r + 1]].copy_(records)
+        elif sizes[r]:
+            reqs.append(dist.irecv(out[offs[r]:offs[r + 1]], src=r, group=group))
+    for q in reqs:
+        q.wait()
+    return out
 
 
 def frame_blocks(frame):

@@ -137,6 +137,18 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
                            uint32_t* hashes, uint32_t nblocks, uint32_t flags, void* stream);
 
 /*
+ * Frame block records on the device (independent-block frames).
+ * Replaces the record writing of compressBuffer's block loop, src/buffer/bufferCompress.js:209-239:
+ * block b's record goes to frame[rec_off[b] ..): LE32 comp_len[b] and the compressed bytes
+ * comp[comp_off[b] ..) when 0 < comp_len[b] < raw_len[b], else LE32 (raw_len[b] | 0x80000000) and the
+ * raw bytes raw[raw_off[b] ..). rec_off is the exclusive prefix sum of the record sizes (4 + payload).
+ * Device pointers only (flags must include LZ4MI_DEVICE_PTRS); async on `stream`.
+ */
+int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len, const uint8_t* comp,
+                         const uint64_t* comp_off, const uint32_t* comp_len, uint8_t* frame, const uint64_t* rec_off,
+                         uint32_t nblocks, uint32_t flags, void* stream);
+
+/*
  * Synthetic input generator (bench/test support, not a reference interface):
  * block b = generator `kind` with seed seed0 + b, block_size bytes each,
  * written to out[b * block_size ..] (device pointer, async on stream).

@@ -239,3 +239,32 @@ def test_full_size_digest_manifest(manifest, kind):
         assert int(st[k]) == 0 and int(dlen[k]) == bs
         assert "%08x" % (int(dh[k]) & 0xFFFFFFFF) == r["js_dec_xxh"] == r["src_xxh"]
     assert torch.equal(dec, raw)
+
+
+def test_frame_pack_matches_reference_frame():
+    """Device-side frame records (lz4mi_frame_pack) == the reference frame's block records."""
+    import torch
+    from lz4mi import shard
+    data = np.concatenate([O.generate("tiles216", 8, 600000), O.generate("random", 9, 70000)])
+    bsize = 65536
+    ref = O.compress_frame(data, None, bsize, True, False, True)
+    info, blocks = shard.frame_blocks(ref)
+    first = blocks[0][0] - 4
+    nb = len(blocks)
+    raw = torch.from_numpy(data.copy()).cuda()
+    raw_off = torch.arange(nb, dtype=torch.int64, device="cuda") * bsize
+    raw_len = torch.tensor([min(bsize, data.size - b * bsize) for b in range(nb)], dtype=torch.int32, device="cuda")
+    slot = (lz4mi.compress_bound(bsize) + 255) & ~255
+    comp = torch.empty(nb * slot, dtype=torch.uint8, device="cuda")
+    comp_off = torch.arange(nb, dtype=torch.int64, device="cuda") * slot
+    comp_len = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    lz4mi.compress_blocks_dev(raw.data_ptr(), raw_off.data_ptr(), raw_len.data_ptr(), comp.data_ptr(),
+                              comp_off.data_ptr(), comp_len.data_ptr(), nb, s)
+    rec = shard.record_sizes(comp_len, raw_len)
+    rec_off = torch.cumsum(rec, 0) - rec
+    out = torch.zeros(int(rec.sum().item()), dtype=torch.uint8, device="cuda")
+    lz4mi.frame_pack_dev(raw.data_ptr(), raw_off.data_ptr(), raw_len.data_ptr(), comp.data_ptr(), comp_off.data_ptr(),
+                         comp_len.data_ptr(), out.data_ptr(), rec_off.data_ptr(), nb, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref[first:ref.size - 4])

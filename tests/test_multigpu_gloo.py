@@ -57,6 +57,12 @@ def _worker(rank, world, port, q):
         local = np.concatenate(outs) if outs else np.zeros(0, dtype=np.uint8)
         back = shard.gather_frame(local, b"", b"")[:-4]        # reuse the gather: no header, EndMark stripped
         ok_back = bool(np.array_equal(back, data))
+        # records gathered to rank 0 by byte counts + point-to-point (the RCCL path's code)
+        import torch
+        got = shard.gather_records_to_root(torch.from_numpy(recs.copy()), root=0)
+        if rank == 0:
+            body = ref[first:ref.size - 8]                      # records between the header and EndMark+checksum
+            ok_frame = ok_frame and bool(np.array_equal(got.numpy(), body))
         q.put((rank, ok_frame, ok_back, int(info["independent"])))
         dist.barrier()
         dist.destroy_process_group()
