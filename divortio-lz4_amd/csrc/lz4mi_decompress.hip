@@ -74,7 +74,7 @@ constexpr int kPad = 64;                      // lookahead for sequences straddl
 constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular sequence may touch
 constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
 constexpr int kMaxSeq = kChunk / 3 + 4;       // every non-final sequence is >= 3 bytes
-constexpr uint32_t kWarm = 256;               // speculative walks start this far before their segment
+constexpr uint32_t kWarm = 512;               // speculative walks start this far before their segment
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
@@ -86,10 +86,18 @@ constexpr int kShortPeriodBulk = 1024;        // longer runs of a < 16-byte peri
 
 struct DecShared {
     uint32_t stage[kStageWords];
-    uint32_t t_out[kMaxSeq];      // output start of each sequence (block-relative)
-    uint2 t_info[kMaxSeq];        // {literal source (chunk-relative) | literal length << 16,
-                                  //  match offset | match length << 16 (0: final literal-only sequence)}
-    int32_t t_rsrc[kMaxSeq];      // round 1: a match's source mapped back to finished output (remap_src)
+    union {
+        struct {
+            uint32_t t_out[kMaxSeq];      // output start of each sequence (block-relative)
+            int32_t t_rsrc[kMaxSeq];      // round 1: a match's source mapped back to finished output (remap_src)
+        };
+        uint16_t nxt4[kChunk];            // parse: token 4 steps after p (warm-up walks)
+    };
+    union {
+        uint2 t_info[kMaxSeq];            // {literal source (chunk-relative) | literal length << 16,
+                                          //  match offset | match length << 16 (0: final literal-only sequence)}
+        uint16_t nxt2[kChunk];            // parse: token 2 steps after p
+    };
     union {
         uint16_t nxt[kLim];       // parse: next-token table
         uint32_t pme[kLim / 2];   // output: ends of the pending matches
@@ -173,6 +181,17 @@ __device__ __forceinline__ uint32_t next_fast(const uint8_t* s, uint32_t p, uint
     if (x1 && p + 1 >= (uint32_t)kLim) v = kStop;
     slow = (x1 && b1 == 255) || (x2 && mb == 255 && q < rem);
     return v;
+}
+
+// Registers loaded by global loads that an explicit wait_vmem() has already
+// covered: redefine them opaquely so the compiler's wait insertion no longer
+// tracks them (it would otherwise wait for every later store before their use).
+__device__ __forceinline__ void settle(uint4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
+__device__ __forceinline__ uint16_t enc_next(uint32_t v) {
+    return (uint16_t)(v == kEnd ? 0xFFFEu : v == kStop ? 0xFFFFu : v);
 }
 
 __device__ __forceinline__ uint32_t next_of(const uint16_t* nxt, uint32_t p) {
@@ -775,6 +794,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         if (!have_pf) {
             pf0 = stage_piece(c, (int64_t)c.ip + 16 * lane);
             if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, (int64_t)c.ip + 16 * (kWave + lane));
+            settle(pf0);
+            settle(pf1);
         }
         have_pf = false;
         __builtin_memcpy((uint8_t*)S.stage + 16 * lane, &pf0, 16);
@@ -786,13 +807,35 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         PROF(0);
         // ---- 2. next-token table -----------------------------------------
         uint16_t* nxt = S.nxt;
-        for (uint32_t p = lane; p < (uint32_t)kLim; p += kWave) {
-            bool slow;
-            uint32_t v = next_fast(s, p, rem, slow);
-            if (__ballot(slow)) {
-                if (slow) v = next_token(s, p, rem);
+        {   // all positions' fields read at once; the rare longer length fields afterwards
+            static_assert(kLim % kWave == 0 && kChunk % kWave == 0, "whole rows per lane");
+            uint32_t slm = 0;
+#pragma unroll
+            for (int i = 0; i < kLim / kWave; ++i) {
+                bool slow;
+                const uint32_t v = next_fast(s, lane + kWave * i, rem, slow);
+                slm |= (slow ? 1u : 0u) << i;
+                nxt[lane + kWave * i] = enc_next(v);
             }
-            nxt[p] = (uint16_t)(v == kEnd ? 0xFFFEu : v == kStop ? 0xFFFFu : v);
+            if (__ballot(slm != 0)) {
+                for (uint32_t m = slm; m; m &= m - 1) {
+                    const uint32_t p = lane + kWave * __builtin_ctz(m);
+                    nxt[p] = enc_next(next_token(s, p, rem));
+                }
+            }
+        }
+        __syncthreads();
+        // 2- and 4-step jumps (the warm-up walks only need where the chain lands)
+#pragma unroll
+        for (int i = 0; i < kChunk / kWave; ++i) {
+            const uint32_t a = nxt[lane + kWave * i];
+            S.nxt2[lane + kWave * i] = a < (uint32_t)kChunk ? nxt[a] : (uint16_t)a;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kChunk / kWave; ++i) {
+            const uint32_t a = S.nxt2[lane + kWave * i];
+            S.nxt4[lane + kWave * i] = a < (uint32_t)kChunk ? S.nxt2[a] : (uint16_t)a;
         }
         __syncthreads();
 #if LZ4MI_ABLATE == 3
@@ -807,6 +850,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         uint32_t vis = 0, x;
         {   // warm-up walk; lanes whose warm-up would start before the chunk start at it, a true token
             uint32_t p = seg0 < kWarm ? 0u : seg0 - kWarm;
+            for (uint32_t q; (q = S.nxt4[p]) < seg0;) p = q;    // jumps stay short of the segment
+            for (uint32_t q; (q = S.nxt2[p]) < seg0;) p = q;
             while (p < seg1) {
                 if (p >= seg0) vis |= 1u << (p - seg0);
                 p = next_of(nxt, p);
@@ -842,6 +887,13 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         const int last_lane = 63 - __builtin_clzll(has);
         const uint32_t last_tok = uniform(__shfl(seg0 + 31 - __builtin_clz(vis | 1u), last_lane, kWave));
         const bool cut = tail == kStop;
+        if (!cut && tail < kEnd && (int64_t)c.ip + tail < c.in_len) {
+            // the next chunk's bytes: loaded while this chunk's table is built
+            const int64_t nip = (int64_t)c.ip + tail;
+            pf0 = stage_piece(c, nip + 16 * lane);
+            if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+            have_pf = true;
+        }
 #if LZ4MI_ABLATE == 2
         c.ip = tail == kEnd ? c.in_len : c.ip + (cut ? kChunk : (int32_t)tail);
         __syncthreads();
@@ -952,9 +1004,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
             cq = q;
         }
         const int64_t tab_hi = c.O + total;
-        {   // the next chunk's bytes: their loads go out before this chunk's stores
-            const int64_t nip = cut ? (cq < c.in_len ? cq : c.in_len)
-                                    : (tail >= kEnd ? (int64_t)c.in_len : (int64_t)c.ip + tail);
+        if (cut) {   // the next chunk's bytes: their loads go out before this chunk's stores
+            const int64_t nip = cq < c.in_len ? cq : c.in_len;
             if (nip < c.in_len) {
                 pf0 = stage_piece(c, nip + 16 * lane);
                 if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
@@ -965,6 +1016,11 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
         // ---- 5. output rounds ---------------------------------------------
+        // The previous chunk's stores (read back as history below) and the next
+        // chunk's loads are complete: the stores had the whole parse to drain.
+        wait_vmem();
+        settle(pf0);    // (so the next chunk's stage does not wait for this chunk's stores)
+        settle(pf1);
         // output -> sequence map for remap_src, in the (now idle) next-token table
         uint32_t msh = 4;
         while ((total >> msh) >= kLim) ++msh;
@@ -1096,8 +1152,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         }
 #endif
         PROF(7);
-        wait_vmem();        // this chunk's stores are complete before they are read back
         if (a.f1check) {
+            wait_vmem();    // this chunk's stores are complete before they are read back
             uint32_t dv = 0;
             for (uint32_t k = lane; k < nseq; k += kWave) {
                 const SeqInfo q = seq_info(S, k);
