@@ -122,17 +122,26 @@ struct Ctx {
     int64_t O;            // output start of the current table (block-relative)
 };
 
+// 16 bytes of base[0, len) at r0, zero past len (r0 < len).
+__device__ __forceinline__ uint4 load16_tail(const uint8_t* base, int64_t r0, int64_t len) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    unsigned __int128 x = 0;
+    if (len >= 16) {   // the last 16 bytes, shifted down
+        __builtin_memcpy(&x, base + len - 16, 16);
+        x >>= 8 * (uint32_t)(r0 - (len - 16));
+    } else {
+#pragma unroll 1
+        for (int j = 0; r0 + j < len; ++j) x |= (unsigned __int128)base[r0 + j] << (8 * j);
+    }
+    __builtin_memcpy(&v, &x, 16);
+    return v;
+}
+
 // 16 compressed bytes at block-relative r0 (zero past the block end).
 __device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + 16 <= c.in_len) {
-        __builtin_memcpy(&v, c.blk + r0, 16);
-    } else if (r0 < c.in_len) {
-        uint32_t o[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 16; ++j)
-            if (r0 + j < c.in_len) o[j >> 2] |= (uint32_t)c.blk[r0 + j] << (8 * (j & 3));
-        v = make_uint4(o[0], o[1], o[2], o[3]);
-    }
+    if (r0 + 16 <= c.in_len) __builtin_memcpy(&v, c.blk + r0, 16);
+    else if (r0 < c.in_len) v = load16_tail(c.blk, r0, c.in_len);
     return v;
 }
 
@@ -978,12 +987,11 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
                 if (q + 16 <= c.in_len) {
                     __builtin_memcpy(w, c.blk + q, 16);
                 } else {
-                    for (int t = 0; t < 4; ++t) {
-                        uint32_t v = 0;
-                        for (int u = 0; u < 4; ++u)
-                            if (q + 4 * t + u < c.in_len) v |= (uint32_t)c.blk[q + 4 * t + u] << (8 * u);
-                        w[t] = v;
-                    }
+                    const uint4 t = load16_tail(c.blk, q, c.in_len);
+                    w[0] = t.x;
+                    w[1] = t.y;
+                    w[2] = t.z;
+                    w[3] = t.w;
                 }
                 coff = w[0] & 0xFFFFu;
                 q += 2;
