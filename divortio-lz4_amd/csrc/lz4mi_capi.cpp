@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -16,6 +17,14 @@
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
                                               int32_t*, uint32_t, int, hipStream_t);
+extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
+                                                      const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
+                                                      uint32_t*, int32_t*, uint32_t, hipStream_t);
+extern "C" hipError_t lz4mi_launch_token_map(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                                             uint32_t, const uint32_t*, uint64_t*, uint32_t, uint32_t, hipStream_t);
+extern "C" hipError_t lz4mi_launch_ring_decode(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
+                                               const uint64_t*, const uint32_t*, uint32_t*, int32_t*, const uint32_t*,
+                                               const uint64_t*, uint32_t, uint32_t*, uint32_t, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
@@ -50,7 +59,13 @@ struct Ctx {
     hipStream_t stream = nullptr;
     Scratch in, out, meta, aux;
     Scratch tables;   // batch encoder hash tables (64 KiB per block)
-    std::mutex mu;
+    // two-pass decoder: per-block chunk index, token bitmaps (128 B per 1 KiB chunk), counters
+    Scratch chunk_base, bitmap, stats;
+    std::vector<uint32_t> h_len, h_base;
+    uint32_t* h_pin = nullptr;   // pinned staging for the block lengths of device-pointer calls
+    size_t h_pin_cap = 0;
+    hipEvent_t ring_done = nullptr;   // the two-pass scratch is free once this has fired
+    std::mutex mu, ring_mu;
 };
 
 Ctx g_ctx;
@@ -68,6 +83,98 @@ int32_t ensure_init() {
 }
 
 hipStream_t pick_stream(void* s) { return s ? static_cast<hipStream_t>(s) : g_ctx.stream; }
+
+constexpr uint32_t kRingChunk = 1024;   // lz4mi_decompress_ring.hip kC
+
+// Decoder selection (LZ4MI_DECODER): "auto" (default) = the two-pass ring decoder for
+// blocks compressed at least kRingRatio:1 (long matches: it writes them from LDS), the
+// single-pass kernel for the rest; "ring" = every block through the ring decoder;
+// "single" = the single-pass kernel only.
+constexpr uint32_t kRingRatio = 32;
+int g_ring_mode = -1;
+uint32_t g_ring_ratio = kRingRatio;
+bool ring_enabled() {
+    if (g_ring_mode < 0) {
+        const char* e = std::getenv("LZ4MI_DECODER");
+        g_ring_mode = (e && std::strcmp(e, "single") == 0) ? 0 : 1;
+        g_ring_ratio = (e && std::strcmp(e, "ring") == 0) ? 0u : kRingRatio;
+    }
+    return g_ring_mode == 1;
+}
+
+// Spec-mode decode of a batch whose pointers are all device pointers: the
+// two-pass ring decoder, then the single-pass kernel for the blocks it hands
+// back. h_in_len: the block lengths if the caller has them on the host (else
+// they are read back from the device, one small synchronous copy).
+hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* h_in_len,
+                       uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
+                       uint32_t dict_len, uint32_t* out_len, int32_t* status, uint32_t nblocks, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_ctx.ring_mu);
+    hipError_t e;
+    if (!g_ctx.ring_done) {
+        if ((e = hipEventCreateWithFlags(&g_ctx.ring_done, hipEventDisableTiming)) != hipSuccess) return e;
+    } else if ((e = hipStreamWaitEvent(s, g_ctx.ring_done, 0)) != hipSuccess) {
+        return e;
+    }
+    const uint32_t* lens = h_in_len;
+    if (!lens) {
+        if (g_ctx.h_pin_cap < nblocks) {
+            if (g_ctx.h_pin) (void)hipHostFree(g_ctx.h_pin);
+            g_ctx.h_pin = nullptr;
+            g_ctx.h_pin_cap = 0;
+            if ((e = hipHostMalloc((void**)&g_ctx.h_pin, 4ull * nblocks, 0)) != hipSuccess) return e;
+            g_ctx.h_pin_cap = nblocks;
+        }
+        if ((e = hipMemcpyAsync(g_ctx.h_pin, in_len, 4ull * nblocks, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        lens = g_ctx.h_pin;
+    }
+    g_ctx.h_base.resize(nblocks);
+    uint64_t total = 0;
+    uint32_t maxc = 0;
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        const uint32_t c = (lens[b] + kRingChunk - 1) / kRingChunk;
+        g_ctx.h_base[b] = (uint32_t)total;
+        total += c;
+        maxc = std::max(maxc, c);
+    }
+    if (total >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if ((e = g_ctx.chunk_base.ensure(4ull * nblocks + 64)) != hipSuccess) return e;
+    if ((e = g_ctx.bitmap.ensure(128ull * total + 64)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(g_ctx.chunk_base.p, g_ctx.h_base.data(), 4ull * nblocks, hipMemcpyHostToDevice, s)) !=
+        hipSuccess)
+        return e;
+    uint32_t* stats = nullptr;
+    if (std::getenv("LZ4MI_RING_STATS")) {
+        if (!g_ctx.stats.p) {
+            if ((e = g_ctx.stats.ensure(64)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(g_ctx.stats.p, 0, 64, s)) != hipSuccess) return e;
+        }
+        stats = g_ctx.stats.as<uint32_t>();
+    }
+    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, g_ring_ratio, g_ctx.chunk_base.as<uint32_t>(),
+                                    g_ctx.bitmap.as<uint64_t>(), nblocks, maxc, s)) != hipSuccess)
+        return e;
+    if ((e = lz4mi_launch_ring_decode(in, in_off, in_len, out, out_off, out_cap, out_len, status,
+                                      g_ctx.chunk_base.as<uint32_t>(), g_ctx.bitmap.as<uint64_t>(), g_ring_ratio, stats,
+                                      nblocks, s)) != hipSuccess)
+        return e;
+    if ((e = lz4mi_launch_decompress_pending(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
+                                             status, nblocks, s)) != hipSuccess)
+        return e;
+    return hipEventRecord(g_ctx.ring_done, s);
+}
+
+hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* h_in_len,
+                         uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
+                         uint32_t dict_len, uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode,
+                         hipStream_t s) {
+    if (mode == 0 && ring_enabled())
+        return ring_decode(in, in_off, in_len, h_in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
+                           nblocks, s);
+    return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
+                                   nblocks, mode, s);
+}
 
 // ---- host XXH32 (reference variant by default, see lz4mi_xxh32.hip) -------
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
@@ -95,6 +202,27 @@ const char* lz4mi_status_message(int32_t s) {
         case LZ4MI_ERR_NO_DEVICE: return "lz4mi: no gfx950 (MI355X) device available";
         default: return "lz4mi: unknown status";
     }
+}
+
+// Debug counters of the two-pass decoder (enabled by LZ4MI_RING_STATS=1):
+// [0] chunks whose token bitmap was rebuilt, [1] sequences written directly,
+// [2] blocks handed to the single-pass kernel. Reads and resets.
+// [3..5] why blocks were handed back: malformed token, sequence error, direct-sequence error.
+int32_t lz4mi_debug_ring_stats(uint32_t* out6) {
+    for (int i = 0; i < 6; ++i) out6[i] = 0;
+    if (!g_ctx.stats.p) return LZ4MI_OK;
+    if (hipDeviceSynchronize() != hipSuccess) return LZ4MI_ERR_HIP;
+    if (hipMemcpy(out6, g_ctx.stats.p, 24, hipMemcpyDeviceToHost) != hipSuccess) return LZ4MI_ERR_HIP;
+    if (hipMemset(g_ctx.stats.p, 0, 24) != hipSuccess) return LZ4MI_ERR_HIP;
+    return LZ4MI_OK;
+}
+
+// Decoder selection for tests / tools: mode 0 single-pass only, 1 ring decoder for blocks
+// compressed at least `ratio`:1 (0: every block). Overrides LZ4MI_DECODER.
+int32_t lz4mi_debug_set_decoder(int32_t mode, uint32_t ratio) {
+    g_ring_mode = mode ? 1 : 0;
+    g_ring_ratio = ratio;
+    return LZ4MI_OK;
 }
 
 const char* lz4mi_version(void) { return "lz4mi 0.1 (gfx950)"; }
@@ -160,8 +288,8 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
-        LZ4MI_TRY(lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
-                                          nblocks, mode, pick_stream(stream)));
+        LZ4MI_TRY(decode_launch(in, in_off, in_len, nullptr, out, out_off, out_cap, dict, dict_len, out_len, status,
+                                nblocks, mode, pick_stream(stream)));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_cap || !out_len || !status) return LZ4MI_ERR_ARG;
@@ -211,9 +339,9 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(lz4mi_launch_decompress(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off,
-                                      m_out_cap, dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status,
-                                      nblocks, mode, s));
+    LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, in_len, g_ctx.out.as<uint8_t>(), m_out_off,
+                            m_out_cap, dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks,
+                            mode, s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));

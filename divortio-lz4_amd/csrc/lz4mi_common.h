@@ -7,32 +7,55 @@ namespace lz4mi {
 
 constexpr int kWave = 64;
 
-// Wave-wide inclusive prefix sum (64 lanes, shuffle-up ladder).
+// Cross-lane steps on DPP (VALU operand modifiers, no LDS round trip): row_shr
+// within rows of 16 lanes, then row_bcast:15 / row_bcast:31 across rows.
+// `old` is what a lane without a source lane receives.
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
+}
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+
+// Wave-wide inclusive prefix sum (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane >= d) v += t;
-    }
+    (void)lane;
+    v += dpp<kRowShr1>(0u, v);
+    v += dpp<kRowShr2>(0u, v);
+    v += dpp<kRowShr4>(0u, v);
+    v += dpp<kRowShr8>(0u, v);
+    v += dpp<kRowBcast15, 0xa>(0u, v);
+    v += dpp<kRowBcast31, 0xc>(0u, v);
     return v;
 }
 
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// Wave-wide minimum / maximum (uniform result).
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        uint32_t t = __shfl_xor(v, d, kWave);
-        v = t < v ? t : v;
-    }
-    return v;
+    const uint32_t F = 0xFFFFFFFFu;
+    v = min(v, dpp<kRowShr1>(F, v));
+    v = min(v, dpp<kRowShr2>(F, v));
+    v = min(v, dpp<kRowShr4>(F, v));
+    v = min(v, dpp<kRowShr8>(F, v));
+    v = min(v, dpp<kRowBcast15, 0xa>(F, v));
+    v = min(v, dpp<kRowBcast31, 0xc>(F, v));
+    return lane63(v);
 }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        uint32_t t = __shfl_xor(v, d, kWave);
-        v = t > v ? t : v;
-    }
-    return v;
+    v = max(v, dpp<kRowShr1>(0u, v));
+    v = max(v, dpp<kRowShr2>(0u, v));
+    v = max(v, dpp<kRowShr4>(0u, v));
+    v = max(v, dpp<kRowShr8>(0u, v));
+    v = max(v, dpp<kRowBcast15, 0xa>(0u, v));
+    v = max(v, dpp<kRowBcast31, 0xc>(0u, v));
+    return lane63(v);
+}
+
+// v of lane l (l uniform).
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }

@@ -19,12 +19,25 @@ struct DecArgs {
     uint32_t nblocks;
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
     int f1check;   // flag blocks the reference's F1 rewrite would change (status kStatusF1)
+    int redo_only; // decode only the blocks whose status is kStatusRedo (handed back by the ring decoder)
 };
 
 constexpr int32_t kStatusF1 = -10;   // internal: block must be decoded by the serial reference-exact kernel
+constexpr int32_t kStatusRedo = -11; // internal: the two-pass ring decoder hands the block to the single-pass kernel
 
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream);
 // Re-decode, one block per workgroup, every block whose status is kStatusF1.
 extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream);
+
+// Two-pass ring decoder (lz4mi_decompress_ring.hip).
+extern "C" hipError_t lz4mi_launch_token_map(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                             const uint32_t* out_cap, uint32_t min_ratio, const uint32_t* chunk_base,
+                                             uint64_t* bitmap, uint32_t nblocks, uint32_t max_chunks,
+                                             hipStream_t stream);
+extern "C" hipError_t lz4mi_launch_ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                               uint32_t* out_len, int32_t* status, const uint32_t* chunk_base,
+                                               const uint64_t* bitmap, uint32_t min_ratio, uint32_t* stats,
+                                               uint32_t nblocks, hipStream_t stream);

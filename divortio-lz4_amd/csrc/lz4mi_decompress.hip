@@ -776,6 +776,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     const int lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
+    if (a.redo_only && a.status[b] != kStatusRedo) return;
 
     Ctx c;
     c.blk = a.in + a.in_off[b];
@@ -1217,4 +1218,17 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || mode != 2) return e;
     return lz4mi_launch_decompress_redo(a, stream);
+}
+
+// Re-decode every block the two-pass ring decoder handed back (status kStatusRedo),
+// with the full semantics of the single-pass kernel (spec mode).
+extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                      uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                                      const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
+                                                      int32_t* status, uint32_t nblocks, hipStream_t stream) {
+    lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
+                     nblocks > 1 ? 1 : 0, 0, 1};
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    return hipGetLastError();
 }
