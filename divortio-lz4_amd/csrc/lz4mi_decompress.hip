@@ -137,6 +137,16 @@ __device__ __forceinline__ uint4 load16_tail(const uint8_t* base, int64_t r0, in
     return v;
 }
 
+// Bytes [idx, idx + 16) of the staged chunk from five naturally aligned dword
+// reads: a misaligned b64/b128 LDS access replays at ~64 LDS cycles, CU-wide
+// (tools/probe/lds_unaligned.hip), aligned dwords do not.
+__device__ __forceinline__ uint4 stage16(const uint32_t* stage, int32_t idx) {
+    const uint32_t* w = stage + (idx >> 2);
+    const uint32_t sh = (uint32_t)idx & 3u;
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    return make_uint4(funnel(d0, d1, sh), funnel(d1, d2, sh), funnel(d2, d3, sh), funnel(d3, d4, sh));
+}
+
 // 16 compressed bytes at block-relative r0 (zero past the block end).
 __device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
     uint4 v = make_uint4(0, 0, 0, 0);
@@ -415,7 +425,7 @@ template <uint32_t KIND>
 __device__ __forceinline__ uint4 load16(const Ctx& c, const DecShared& S, int32_t a) {
     uint4 v;
     if (KIND == R_LDS) {
-        __builtin_memcpy(&v, (const uint8_t*)S.stage + a, 16);
+        v = stage16(S.stage, a);
     } else if (KIND == R_COMP) {
         __builtin_memcpy(&v, c.blk + a, 16);
     } else {
@@ -689,9 +699,8 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
     const int np = n >= 16 ? (n + 15) >> 4 : 0;
     for (int q = 0; __ballot(q < np) != 0; q += 2) {       // runs of >= 16 bytes: 16-byte pieces
         const int32_t d0 = 16 * q < n - 16 ? 16 * q : n - 16, d1 = 16 * (q + 1) < n - 16 ? 16 * (q + 1) : n - 16;
-        uint4 v0, v1;
-        __builtin_memcpy(&v0, (const uint8_t*)S.stage + L.src + d0, 16);
-        __builtin_memcpy(&v1, (const uint8_t*)S.stage + L.src + d1, 16);
+        const uint4 v0 = stage16(S.stage, L.src + d0);
+        const uint4 v1 = stage16(S.stage, L.src + d1);
         if (LZ4MI_ABLATE == 4) continue;
         if (q < np) __builtin_memcpy(c.dst + L.y + d0, &v0, 16);
         if (q + 1 < np) __builtin_memcpy(c.dst + L.y + d1, &v1, 16);
@@ -699,9 +708,8 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
     if (__ballot(n > 0 && n < 16)) {                       // shorter runs: two overlapping 8/4/2/1-byte stores
         if (n > 0 && n < 16) {
             const uint32_t w = n >= 8 ? 8u : n >= 4 ? 4u : n >= 2 ? 2u : 1u;
-            uint4 v0, v1;
-            __builtin_memcpy(&v0, (const uint8_t*)S.stage + L.src, 16);
-            __builtin_memcpy(&v1, (const uint8_t*)S.stage + L.src + n - (int32_t)w, 16);
+            const uint4 v0 = stage16(S.stage, L.src);
+            const uint4 v1 = stage16(S.stage, L.src + n - (int32_t)w);
             if (LZ4MI_ABLATE != 4) {
                 store_w(c.dst + L.y, v0, w);
                 store_w(c.dst + L.y + n - (int32_t)w, v1, w);
