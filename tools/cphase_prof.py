@@ -44,6 +44,10 @@ def main():
             print(f"{gen} blocks={n} kernel_ms={ms:.1f} iters/block={it:.0f} hits/block={v[9] / n:.0f} "
                   f"wave_ms={sum(v[:7]) / 100.0 / n / 1000:.1f}")
             print("   ns/iteration:", per, flush=True)
+            gt = ["head probe", "verify", "extend", "miss batch"]
+            print("   GT encoder: ns/head-probe", {gt[i]: round(v[i] / 100.0 / max(1, v[8]) * 1000, 1) for i in range(4)},
+                  "per block: head probes", round(v[8] / n), "speculated", round(v[9] / n), "hits", round(v[10] / n),
+                  "miss batches", round(v[11] / n), "emit ns/hit", round(v[12] * 10 / max(1, v[10])), "hit-check wait ns/hit", round(v[13] * 10 / max(1, v[10])), flush=True)
             del raw, comp
             torch.cuda.empty_cache()
 
