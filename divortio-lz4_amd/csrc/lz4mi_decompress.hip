@@ -83,6 +83,7 @@ constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 128;               // longer runs are written by the whole wave
 constexpr int kShortPeriodBulk = 1024;        // longer runs of a < 16-byte period use the LDS phase table
+constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
 
 struct DecShared {
     uint32_t stage[kStageWords];
@@ -667,6 +668,26 @@ __device__ __forceinline__ void short_period_run(const Ctx& c, DecShared& S, int
     __syncthreads();
 }
 
+// A long literal run (incompressible data: one run per block) copied global ->
+// global with 4 16-byte pieces per lane in flight (4 KiB per wave), enough to
+// keep HBM busy with one wave per block; the last piece overlaps its predecessor.
+__device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, int32_t n, int lane) {
+    const int32_t np = (n + 15) >> 4;
+    auto at = [&](int32_t p) { return 16 * p < n - 16 ? 16 * p : n - 16; };   // past the end: the last piece again
+    for (int32_t p0 = lane; p0 < np; p0 += kWave * 4) {
+        const int32_t d0 = at(p0), d1 = at(p0 + kWave), d2 = at(p0 + 2 * kWave), d3 = at(p0 + 3 * kWave);
+        uint4 v0, v1, v2, v3;
+        __builtin_memcpy(&v0, src + d0, 16);
+        __builtin_memcpy(&v1, src + d1, 16);
+        __builtin_memcpy(&v2, src + d2, 16);
+        __builtin_memcpy(&v3, src + d3, 16);
+        __builtin_memcpy(dst + d0, &v0, 16);
+        __builtin_memcpy(dst + d1, &v1, 16);
+        __builtin_memcpy(dst + d2, &v2, 16);
+        __builtin_memcpy(dst + d3, &v3, 16);
+    }
+}
+
 // The whole wave writes one run (uniform R).
 __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
     if (R.kind == R_NONE || R.n <= 0) return;
@@ -689,6 +710,7 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
     }
     WaveGen<kWaveB> g{R, np, 0, lane};
     if (R.kind == R_LDS) pipe<R_LDS, false, kWaveB>(c, S, g);
+    else if (R.kind == R_COMP && R.n >= kLongLit) long_literals(c.dst + R.y, c.blk + R.src, R.n, lane);
     else if (R.kind == R_COMP) pipe<R_COMP, false, kWaveB>(c, S, g);
     else pipe<R_HIST, false, kWaveB>(c, S, g);
 }
