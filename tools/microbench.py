@@ -49,7 +49,15 @@ def main():
     res = {}
     for gen in args.gens.split(","):
         raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-        lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+        if gen == "mix":   # bench.py's 50/50 random/tiles216 mix (same shuffle)
+            sys.path.insert(0, ROOT)
+            from bench import mix_order
+            tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+            for b, kind in enumerate(mix_order(n)):
+                lz4mi.generate_blocks_dev(tmp.data_ptr(), kind, 1 + b, BLOCK, 1, sp)
+                raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+        else:
+            lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
         slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
         comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
         roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
