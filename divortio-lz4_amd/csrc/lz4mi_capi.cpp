@@ -19,7 +19,8 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, c
                                               int32_t*, uint32_t, int, hipStream_t);
 extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                       const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
-                                                      uint32_t*, int32_t*, uint32_t, hipStream_t);
+                                                      uint32_t*, int32_t*, uint32_t, const uint64_t*, const uint32_t*,
+                                                      hipStream_t);
 extern "C" hipError_t lz4mi_launch_token_map(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                                              uint32_t, const uint32_t*, uint64_t*, uint32_t, uint32_t, hipStream_t);
 extern "C" hipError_t lz4mi_launch_ring_decode(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
@@ -152,7 +153,9 @@ hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t
         }
         stats = g_ctx.stats.as<uint32_t>();
     }
-    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, g_ring_ratio, g_ctx.chunk_base.as<uint32_t>(),
+    // LZ4MI_BITMAP=1: pass 1 maps every block and the single-pass kernel takes its token starts from it
+    static const bool bm_mode = std::getenv("LZ4MI_BITMAP") && std::getenv("LZ4MI_BITMAP")[0] == '1';
+    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, bm_mode ? 0u : g_ring_ratio, g_ctx.chunk_base.as<uint32_t>(),
                                     g_ctx.bitmap.as<uint64_t>(), nblocks, maxc, s)) != hipSuccess)
         return e;
     if ((e = lz4mi_launch_ring_decode(in, in_off, in_len, out, out_off, out_cap, out_len, status,
@@ -160,7 +163,8 @@ hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t
                                       nblocks, s)) != hipSuccess)
         return e;
     if ((e = lz4mi_launch_decompress_pending(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
-                                             status, nblocks, s)) != hipSuccess)
+                                             status, nblocks, bm_mode ? g_ctx.bitmap.as<uint64_t>() : nullptr,
+                                             g_ctx.chunk_base.as<uint32_t>(), s)) != hipSuccess)
         return e;
     return hipEventRecord(g_ctx.ring_done, s);
 }

@@ -20,6 +20,8 @@ struct DecArgs {
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
     int f1check;   // flag blocks the reference's F1 rewrite would change (status kStatusF1)
     int redo_only; // decode only the blocks whose status is kStatusRedo (handed back by the ring decoder)
+    const uint64_t* bitmap;      // token bitmaps of pass 1 (lz4mi_token_map_kernel): replace the speculative parse
+    const uint32_t* chunk_base;  // first bitmap chunk of each block
 };
 
 constexpr int32_t kStatusF1 = -10;   // internal: block must be decoded by the serial reference-exact kernel

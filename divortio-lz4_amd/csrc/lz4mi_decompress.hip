@@ -801,7 +801,11 @@ __device__ __forceinline__ uint32_t f1_changes(const Ctx& c, int32_t ms, int32_t
     return 0;
 }
 
-__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
+// BM: the chunk's token starts come from pass 1's bitmap (lz4mi_decompress_ring.hip)
+// instead of the next-token table / jump tables / speculative walks; chunks are then
+// the fixed 1 KiB chunks of the bitmap, staged from their base.
+template <bool BM>
+__device__ __forceinline__ void decompress_block(const DecArgs& a) {
     __shared__ DecShared S;
     const int lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -822,6 +826,9 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     int32_t status = 0;
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
     bool have_pf = false;
+    int64_t pf_at = -1;                    // compressed position pf0/pf1 were loaded from
+    uint32_t pfm = 0;                      // (BM) the bitmap bits of the prefetched chunk, this lane's segment
+    const uint16_t* bm16 = BM ? (const uint16_t*)(a.bitmap + (uint64_t)a.chunk_base[b] * (kChunk / 64)) : nullptr;
 #if LZ4MI_PROFILE
     uint64_t prof[24] = {0};
     uint64_t prof_t = wall_clock64();
@@ -829,11 +836,14 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 
     while (c.ip < c.in_len) {
         PROF_COUNT(10, 1);
+        const int32_t entry = c.ip;               // the true next token
+        if (BM) c.ip = entry & ~(kChunk - 1);     // stage from the chunk's base
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
         // the previous chunk's output phase, ahead of its stores) -------------
-        if (!have_pf) {
+        if (!have_pf || pf_at != c.ip) {
             pf0 = stage_piece(c, (int64_t)c.ip + 16 * lane);
             if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, (int64_t)c.ip + 16 * (kWave + lane));
+            if (BM) pfm = bm16[(c.ip / kChunk) * 64 + lane];
             settle(pf0);
             settle(pf1);
         }
@@ -844,6 +854,46 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         const uint8_t* s = (const uint8_t*)S.stage;
         const uint32_t rem = (uint32_t)(c.in_len - c.ip);
 
+        const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
+        uint32_t vis, tail;
+        if (BM) {
+            PROF(0);
+            // ---- 2-3. the chunk's tokens from pass 1's bitmap, from the true entry on
+            const uint32_t rel = (uint32_t)(entry - c.ip);
+            vis = pfm & 0xFFFFu;
+            if (seg0 + 16 <= rel) vis = 0;
+            else if (seg0 < rel) vis &= ~((1u << (rel - seg0)) - 1u);
+            if (!__ballot(lane == (int)(rel >> 4) && ((vis >> (rel & 15)) & 1u))) {
+                // pass 1's walk was off the true chain at the entry: walk the true chain
+                // until it lands on a token of pass 1's walk (from there on they coincide)
+                S.nxt[lane] = (uint16_t)vis;
+                S.nxt[64 + lane] = 0;
+                __syncthreads();
+                if (lane == 0) {
+                    uint32_t p = rel;
+                    while (p < (uint32_t)kChunk && p < rem) {
+                        if ((S.nxt[p >> 4] >> (p & 15)) & 1u) break;
+                        S.nxt[64 + (p >> 4)] |= (uint16_t)(1u << (p & 15));
+                        const uint32_t q = next_token(s, p, rem);
+                        if (q >= kEnd) {   // the last token of the chunk: nothing of pass 1's after it
+                            p = kChunk;
+                            break;
+                        }
+                        p = q;
+                    }
+                    S.nxt[128] = (uint16_t)(p < (uint32_t)kChunk ? p : (uint32_t)kChunk);
+                }
+                __syncthreads();
+                const uint32_t ps = S.nxt[128];
+                if (seg0 + 16 <= ps) vis = 0;
+                else if (seg0 < ps) vis &= ~((1u << (ps - seg0)) - 1u);
+                vis |= S.nxt[64 + lane];
+                __syncthreads();
+            }
+            const uint64_t hv = __ballot(vis != 0);
+            const uint32_t lt = lane_val(seg0 + 31 - __builtin_clz(vis | 1u), (uint32_t)(63 - __builtin_clzll(hv)));
+            tail = uniform(next_token(s, lt, rem));   // where the chain leaves the chunk
+        } else {
         PROF(0);
         // ---- 2. next-token table -----------------------------------------
         uint16_t* nxt = S.nxt;
@@ -886,8 +936,8 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
 
         PROF(1);
         // ---- 3. speculative walks + certification -------------------------
-        const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
-        uint32_t vis = 0, x;
+        uint32_t x;
+        vis = 0;
         {   // warm-up walk; lanes whose warm-up would start before the chunk start at it, a true token
             uint32_t p = seg0 < kWarm ? 0u : seg0 - kWarm;
             for (uint32_t q; (q = S.nxt4[p]) < seg0;) p = q;    // jumps stay short of the segment
@@ -922,16 +972,21 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         }
         if (nE >= seg1) vis = 0;
         else vis &= ~((1u << (nE - seg0)) - 1u);
-        const uint32_t tail = uniform(__shfl(x, kWave - 1, kWave));   // where the chain leaves the chunk
+        tail = uniform(__shfl(x, kWave - 1, kWave));   // where the chain leaves the chunk
+        }
+        (void)seg1;
         const uint64_t has = __ballot(vis != 0);
         const int last_lane = 63 - __builtin_clzll(has);
-        const uint32_t last_tok = uniform(__shfl(seg0 + 31 - __builtin_clz(vis | 1u), last_lane, kWave));
+        const uint32_t last_tok = lane_val(seg0 + 31 - __builtin_clz(vis | 1u), (uint32_t)last_lane);
         const bool cut = tail == kStop;
         if (!cut && tail < kEnd && (int64_t)c.ip + tail < c.in_len) {
             // the next chunk's bytes: loaded while this chunk's table is built
-            const int64_t nip = (int64_t)c.ip + tail;
+            int64_t nip = (int64_t)c.ip + tail;
+            if (BM) nip &= ~(int64_t)(kChunk - 1);
             pf0 = stage_piece(c, nip + 16 * lane);
             if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+            if (BM) pfm = bm16[(nip / kChunk) * 64 + lane];
+            pf_at = nip;
             have_pf = true;
         }
 #if LZ4MI_ABLATE == 2
@@ -1044,10 +1099,13 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
         }
         const int64_t tab_hi = c.O + total;
         if (cut) {   // the next chunk's bytes: their loads go out before this chunk's stores
-            const int64_t nip = cq < c.in_len ? cq : c.in_len;
+            int64_t nip = cq < c.in_len ? cq : c.in_len;
             if (nip < c.in_len) {
+                if (BM) nip &= ~(int64_t)(kChunk - 1);
                 pf0 = stage_piece(c, nip + 16 * lane);
                 if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+                if (BM) pfm = bm16[(nip / kChunk) * 64 + lane];
+                pf_at = nip;
                 have_pf = true;
             }
         }
@@ -1224,6 +1282,9 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) {
     }
 }
 
+__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block<false>(a); }
+__global__ __launch_bounds__(64, 4) void lz4mi_decompress_bm_kernel(DecArgs a) { decompress_block<true>(a); }
+
 }  // namespace lz4mi
 
 #if LZ4MI_PROFILE
@@ -1255,10 +1316,12 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
 extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                       uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                                       const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
-                                                      int32_t* status, uint32_t nblocks, hipStream_t stream) {
+                                                      int32_t* status, uint32_t nblocks, const uint64_t* bitmap,
+                                                      const uint32_t* chunk_base, hipStream_t stream) {
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
-                     nblocks > 1 ? 1 : 0, 0, 1};
+                     nblocks > 1 ? 1 : 0, 0, 1, bitmap, chunk_base};
     if (nblocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    if (bitmap) hipLaunchKernelGGL(lz4mi::lz4mi_decompress_bm_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    else hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
