@@ -37,6 +37,10 @@
 #include "lz4mi_common.h"
 #include "lz4mi_decompress.h"
 
+#ifndef LZ4MI_RING_ABLATE
+#define LZ4MI_RING_ABLATE 0   // timing-only variants: 1 = sources always ready, 2 = no unit phase
+#endif
+
 #ifndef LZ4MI_RING_PROFILE
 #define LZ4MI_RING_PROFILE 0   // timing-only variant (tools/ring_prof.py): per-phase wall-clock accumulation
 #endif
@@ -605,6 +609,7 @@ __device__ __noinline__ uint4 make_unit(const RingShared& S, const Step& st, int
     const int32_t end = U + 16 < st.B ? U + 16 : st.B;
     int32_t pos = U;
     auto ready = [&](int32_t s, int32_t e) -> bool {   // bytes [s, e) of earlier output are complete
+        if (LZ4MI_RING_ABLATE & 1) return true;
         const int32_t lo = s > bU0 ? s : bU0;
         if (e <= lo || e <= st.A) return true;
         const int32_t u0 = (lo - bU0) >> 4, u1 = (e - 1 - bU0) >> 4;
@@ -739,7 +744,7 @@ __device__ __forceinline__ uint4 fast_unit(const RingShared& S, const Step& st, 
     }
     const int32_t lim = bU0 > st.A ? bU0 : st.A;
     auto waits = [&](int32_t rs, int32_t re) -> bool {
-        if (re <= rs) return false;
+        if (re <= rs || (LZ4MI_RING_ABLATE & 1)) return false;
         if (repass && rs < bU0 + 16 * kThreads - kRing + 16) slow = true;   // maybe overwritten: general path
         if (re <= lim) return false;
         const int32_t u0 = ((rs > lim ? rs : lim) - bU0) >> 4, u1 = (re - 1 - bU0) >> 4;
@@ -928,7 +933,7 @@ __global__ __launch_bounds__(kThreads, 2) void lz4mi_ring_decode_kernel(RingArgs
         RPROF(3);
 
         // ---- output units, kThreads per batch, in position order
-        for (int32_t bu = 0; bu < nunits; bu += kThreads) {
+        for (int32_t bu = 0; bu < ((LZ4MI_RING_ABLATE & 2) ? 0 : nunits); bu += kThreads) {
             const int32_t r = bu + tid;
             const int32_t U = st.A0 + 16 * r;
             const int32_t bU0 = st.A0 + 16 * bu;

@@ -1,7 +1,8 @@
 """Multi-GPU sharding of independent LZ4 frame blocks.
 
 One process per GPU. Independent blocks need no exchange to be compressed or
-decoded: each rank takes its own range (`shard_range`). The frame is the one
+decoded: each rank takes its own range (`shard_range`), or every world-th block
+(`shard_interleaved`) when per-block cost is clustered by position. The frame is the one
 real exchange step: the compressed blocks of all ranks are concatenated, in
 block order, between the header and the EndMark. `gather_frame` does that with
 two collectives over `torch.distributed` (RCCL over xGMI with the nccl backend,
@@ -29,6 +30,20 @@ def shard_range(nblocks, rank, world):
     per = -(-nblocks // world)
     lo = min(nblocks, rank * per)
     return lo, min(nblocks, lo + per)
+
+
+def shard_interleaved(nblocks, rank, world):
+    """Global block indices of `rank` under interleaved assignment (b = rank, rank + world, ...).
+
+    For batches whose per-block cost is skewed by position (a clustered random/tiles216 mix,
+    where a contiguous split would give one rank all the cheap blocks), every rank gets the same share of
+    each cluster. Blocks stay independent: each decodes into its own output slot, no exchange."""
+    return list(range(rank, nblocks, world)) if 0 <= rank < world else []
+
+
+def clustered_mix_kinds(nblocks):
+    """SURVEY.md §8d config (5), clustered variant: the first half random blocks, then tiles216."""
+    return ["random"] * (nblocks // 2) + ["tiles216"] * (nblocks - nblocks // 2)
 
 
 def block_records(raw_blocks, comp_blocks):

@@ -78,6 +78,17 @@ def test_shard_range_covers_blocks():
             assert got == list(range(n))
 
 
+def test_shard_interleaved_balances_clustered_mix():
+    from lz4mi import shard
+    for n in (0, 1, 7, 16, 4096):
+        for w in (1, 2, 3, 8):
+            parts = [shard.shard_interleaved(n, r, w) for r in range(w)]
+            assert sorted(b for p in parts for b in p) == list(range(n))
+            kinds = shard.clustered_mix_kinds(n)
+            rnd = [sum(kinds[b] == "random" for b in p) for p in parts]
+            assert max(rnd) - min(rnd) <= 1 + (n % w != 0)   # each rank gets an even share of each cluster
+
+
 def test_frame_gather_and_sharded_decode_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
