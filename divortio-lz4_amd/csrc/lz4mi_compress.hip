@@ -802,7 +802,7 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
     a.nblocks = nblocks;
     // encoder: LZ4MI_ENCODER=lds selects the LDS-table kernel (4 blocks per CU);
     // default: global tables (16 blocks per CU; `tables` = 64 KiB per block of scratch)
-    static const char* enc = getenv("LZ4MI_ENCODER");
+    const char* enc = getenv("LZ4MI_ENCODER");   // read per call: tools/compress_ab.py switches it in-process
     if (enc && enc[0] == 'l') {
         hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
         return hipGetLastError();
