@@ -39,7 +39,28 @@ __global__ __launch_bounds__(256) void lz4mi_xxh32_kernel(const uint8_t* in, con
     uint32_t v = init[j];
     const uint8_t* q = p + 4 * j;
     uint64_t k = 0;
-    for (; k + 8 <= stripes; k += 8) {
+    // software pipeline: the next kDepth stripes' words are in flight while the
+    // current kDepth are folded into the accumulator (one load round trip per
+    // 2 x kDepth stripes would otherwise stall the serial chain every kDepth steps)
+    constexpr int kDepth = 128;
+    if (stripes >= 2 * kDepth) {
+        uint32_t w[kDepth];
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) w[u] = load_le32(q + 16 * u, aligned);
+        for (; k + 2 * kDepth <= stripes; k += kDepth) {
+            uint32_t nw[kDepth];
+#pragma unroll
+            for (int u = 0; u < kDepth; ++u) nw[u] = load_le32(q + 16 * (k + kDepth + u), aligned);
+#pragma unroll
+            for (int u = 0; u < kDepth; ++u) v = rotl(v + w[u] * P2, 13) * P1;
+#pragma unroll
+            for (int u = 0; u < kDepth; ++u) w[u] = nw[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) v = rotl(v + w[u] * P2, 13) * P1;
+        k += kDepth;
+    }
+    for (; k + 8 <= stripes; k += 8) {   // short buffers and the pipeline's remainder
         uint32_t w[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) w[u] = load_le32(q + 16 * (k + u), aligned);
@@ -136,8 +157,9 @@ __global__ __launch_bounds__(64) void lz4mi_generate_kernel(uint8_t* out, uint32
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
                                          uint32_t* hashes, uint32_t n, int standard, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    // one wave (16 buffers) per workgroup: the waves spread over every CU's load path
     uint32_t threads = n * 4;
-    hipLaunchKernelGGL(lz4mi::lz4mi_xxh32_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, in, off, len, seed,
+    hipLaunchKernelGGL(lz4mi::lz4mi_xxh32_kernel, dim3((threads + 63) / 64), dim3(64), 0, stream, in, off, len, seed,
                        hashes, n, standard);
     return hipGetLastError();
 }

@@ -143,6 +143,19 @@ def test_xxh32_batch_matches_reference(manifest):
         assert a == O.xxh32_std(base[:n])
 
 
+def test_xxh32_batch_pipeline_edges():
+    """Lengths around the kernel's 128-stripe load pipeline (2 x 128 x 16 B) and its
+    8-stripe remainder loop, at odd buffer alignments, against the oracle."""
+    src = O.generate("random", 11, (1 << 16) + 64)
+    lens = [0, 15, 16, 4095, 4096, 4097, 4111, 4112, 4128, 6144 + 7, 8191, 8192, 8193, 12288 + 200,
+            (1 << 16) - 1, 1 << 16, (1 << 16) + 17]
+    bufs = [src[k % 5:k % 5 + n] for k, n in enumerate(lens)]
+    for seed in (0, 12345):
+        hs = lz4mi.xxh32_blocks(bufs, seed)
+        for n, b, h in zip(lens, bufs, hs):
+            assert int(h) == O.xxh32(b, seed), n
+
+
 def test_generator_matches_oracle():
     torch = pytest.importorskip("torch")
     bs = 1 << 20
