@@ -13,6 +13,7 @@
  *
  * Reference citations (paths relative to the reference repo root):
  *   orc_xxh32             src/xxhash32/xxhash32.js:21-98
+ *   orc_xxh32_stateful    src/xxhash32/xxhash32Stateful.js:13-152
  *   orc_compress_block    src/block/blockCompress.js:31-233 (constants :13-17)
  *   orc_decompress_block  src/block/blockDecompress.js:30-275
  *   orc_compress_frame    src/buffer/bufferCompress.js:77-82,100-259
@@ -87,6 +88,49 @@ static uint32_t xxh32_impl(const uint8_t* in, uint64_t len, uint32_t seed, int s
 uint32_t orc_xxh32(const uint8_t* in, uint64_t len, uint32_t seed) { return xxh32_impl(in, len, seed, 0); }
 uint32_t orc_xxh32_std(const uint8_t* in, uint64_t len, uint32_t seed) { return xxh32_impl(in, len, seed, 1); }
 
+/* xxhash32Stateful.js:13-152 — class XXHash32 fed `nchunks` consecutive chunks of
+ * `in` (chunk k is chunk_len[k] bytes): update() carries up to 15 bytes in a
+ * 16-byte memory (:34-68); totalLen is kept as `(totalLen + len) | 0` (:37) and
+ * digest() tests it with a signed `>= 16` (:113), exactly as the class does. */
+uint32_t orc_xxh32_stateful(const uint8_t* in, const uint64_t* chunk_len, uint32_t nchunks, uint32_t seed) {
+    uint32_t v[4] = { seed + P1 + P2, seed + P2, seed, seed - P1 };
+    int32_t total = 0;
+    uint32_t mem_size = 0;
+    uint8_t mem[16];
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint8_t* b = in;
+        const uint64_t len = chunk_len[c];
+        in += len;
+        total = (int32_t)((uint32_t)total + (uint32_t)len);
+        if (mem_size + len < 16) { memcpy(mem + mem_size, b, len); mem_size += (uint32_t)len; continue; }
+        uint64_t p = 0;
+        if (mem_size > 0) {
+            p = 16 - mem_size;
+            memcpy(mem + mem_size, b, p);
+            for (int k = 0; k < 4; ++k) v[k] = rotl32(v[k] + rd32(mem + 4 * k) * P2, 13) * P1;
+            mem_size = 0;
+        }
+        for (; p + 16 <= len; p += 16)
+            for (int k = 0; k < 4; ++k) v[k] = rotl32(v[k] + rd32(b + p + 4 * k) * P2, 13) * P1;
+        if (p < len) { memcpy(mem, b + p, len - p); mem_size = (uint32_t)(len - p); }
+    }
+    uint32_t h;
+    if (total >= 16) {
+        h = rotl32(v[0], 1);
+        h = rotl32(h + v[1], 7);
+        h = rotl32(h + v[2], 12);
+        h = rotl32(h + v[3], 18);
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)total;
+    uint32_t p = 0;
+    for (; p + 4 <= mem_size; p += 4) h = rotl32(h + rd32(mem + p) * P3, 17) * P4;
+    for (; p < mem_size; ++p) h = rotl32(h + mem[p] * P5, 11) * P1;
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+
 /* ------------------------------------------------------- block compressor */
 /* Output sink with JS typed-array semantics (writes past the end dropped). */
 typedef struct { uint8_t* b; int64_t cap; int64_t pos; } sink_t;
@@ -99,9 +143,15 @@ static void put_len_ext(sink_t* s, int32_t extra) {           /* 255-run varint 
 
 /* blockCompress.js:31-233. `table` holds 16384 int32 entries of (absolute
  * position + 1); entries <= 0 mean empty. Positions are absolute in `src`. */
-int32_t orc_compress_block(const uint8_t* src, uint64_t src_total, uint8_t* out, uint64_t out_total,
-                           int32_t src_start, int32_t src_len, int32_t* table, int32_t out_off) {
+/* A literal run longer than 64 bytes is copied with output.set() (:100, :198), which
+ * throws a RangeError when it would run past the end of `output` (shorter runs use
+ * per-byte stores, whose out-of-range writes are dropped). *status = ORC_ERR_RANGE
+ * then; the bytes and table entries written before the throw stay written. */
+int32_t orc_compress_block_ex(const uint8_t* src, uint64_t src_total, uint8_t* out, uint64_t out_total,
+                              int32_t src_start, int32_t src_len, int32_t* table, int32_t out_off,
+                              int32_t* status) {
     (void)src_total;
+    *status = ORC_OK;
     const int32_t end = src_start + src_len;
     const int32_t mflimit = end - 12;      /* MF_LIMIT  :14 */
     const int32_t matchlimit = end - 5;    /* LAST_LITERALS :13 */
@@ -123,6 +173,7 @@ int32_t orc_compress_block(const uint8_t* src, uint64_t src_total, uint8_t* out,
         int64_t tok = s.pos;
         put(&s, (uint8_t)(lit >= 15 ? 0xF0 : (lit << 4)));
         if (lit >= 15) put_len_ext(&s, lit - 15);
+        if (lit > 64 && s.pos + lit > s.cap) { *status = ORC_ERR_RANGE; return (int32_t)(s.pos - out_off); }
         for (int32_t k = 0; k < lit; ++k) put(&s, src[anchor + k]);
         int32_t e = i + 4, m = cand + 4;   /* forward extension only (:147-150) */
         while (e < matchlimit && src[e] == src[m]) { ++e; ++m; }
@@ -141,8 +192,15 @@ int32_t orc_compress_block(const uint8_t* src, uint64_t src_total, uint8_t* out,
     int32_t lit = end - anchor;            /* final literals (:179-230) */
     put(&s, (uint8_t)(lit >= 15 ? 0xF0 : (lit << 4)));
     if (lit >= 15) put_len_ext(&s, lit - 15);
+    if (lit > 64 && s.pos + lit > s.cap) { *status = ORC_ERR_RANGE; return (int32_t)(s.pos - out_off); }
     for (int32_t k = 0; k < lit; ++k) put(&s, src[anchor + k]);
     return (int32_t)(s.pos - out_off);
+}
+
+int32_t orc_compress_block(const uint8_t* src, uint64_t src_total, uint8_t* out, uint64_t out_total,
+                           int32_t src_start, int32_t src_len, int32_t* table, int32_t out_off) {
+    int32_t st;
+    return orc_compress_block_ex(src, src_total, out, out_total, src_start, src_len, table, out_off, &st);
 }
 
 /* ----------------------------------------------------- block decompressor */

@@ -41,6 +41,11 @@ def lib():
         L.orc_xxh32.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
         L.orc_xxh32_std.restype = ctypes.c_uint32
         L.orc_xxh32_std.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_xxh32_stateful.restype = ctypes.c_uint32
+        L.orc_xxh32_stateful.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_compress_block_ex.restype = ctypes.c_int32
+        L.orc_compress_block_ex.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, _i32p]
         L.orc_compress_block.restype = ctypes.c_int32
         L.orc_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
@@ -91,6 +96,15 @@ def xxh32_std(data, seed=0):
     return lib().orc_xxh32_std(_ptr(a), a.size, seed & 0xFFFFFFFF)
 
 
+def xxh32_stateful(chunks, seed=0):
+    """class XXHash32 (xxhash32Stateful.js) fed the given chunks in order."""
+    arrs = [_u8(c) for c in chunks]
+    data = np.concatenate(arrs) if arrs else np.zeros(0, dtype=np.uint8)
+    lens = np.array([a.size for a in arrs], dtype=np.uint64)
+    return lib().orc_xxh32_stateful(_ptr(data), lens.ctypes.data if lens.size else None, lens.size,
+                                    seed & 0xFFFFFFFF)
+
+
 def generate(kind, seed, n):
     """Seeded synthetic input (SURVEY.md §8d generators)."""
     k = GENERATORS[kind] if isinstance(kind, str) else kind
@@ -115,6 +129,17 @@ def compress_block(src, start=0, length=None, table=None, out=None, out_off=0):
     n = lib().orc_compress_block(_ptr(s), s.size, _ptr(out), out.size, start, length,
                                  table.ctypes.data, out_off)
     return n, out, table
+
+
+def compress_raw(src, out, start, length, table, out_off):
+    """compressBlock with the reference's exception: returns (status, written); status
+    -8 (RangeError of output.set, blockCompress.js:100/198) leaves `out`/`table` as
+    the reference leaves them when it throws."""
+    s = _u8(src)
+    st = ctypes.c_int32(0)
+    n = lib().orc_compress_block_ex(_ptr(s), s.size, _ptr(out), out.size, start, length, table.ctypes.data,
+                                    out_off, ctypes.byref(st))
+    return st.value, n
 
 
 def compress_block_bytes(src):

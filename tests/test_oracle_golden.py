@@ -169,3 +169,32 @@ def test_digest_manifest_4mib_subset(manifest, kind):
         assert comp.size == r["comp_len"] and "%08x" % O.xxh32(comp) == r["comp_xxh"]
         st, w, out = O.decompress_block(comp, src.size, js_compat=True)
         assert st == 0 and w == r["js_dec_written"] and "%08x" % O.xxh32(out) == r["js_dec_xxh"]
+
+
+def test_compress_raw_edges(manifest):
+    """F7 (five-argument call returns 0) and the RangeError of output.set on an
+    overflowing literal run > 64 bytes (blockCompress.js:37,100,198,232): the
+    oracle reproduces the reference's output bytes and table at return/throw."""
+    (g,) = cases_of(manifest, "compress_raw_edges")
+    for c in g["cases"]:
+        src = golden_bytes(c["src_file"]).copy()
+        out = np.zeros(c["out_len"], dtype=np.uint8)
+        table = np.zeros(16384, dtype=np.int32)
+        st, n = O.compress_raw(src, out, c["start"], c["len"], table, c["out_off"] or 0)
+        if c["ok"]:
+            assert st == 0, c["name"]
+            assert (0 if c["five_args"] else n) == c["value"], c["name"]
+        else:
+            assert st == -8 and c["error_name"] == "RangeError", c["name"]
+        assert np.array_equal(out, golden_bytes(c["out_file"])), c["name"]
+        assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_file"])), c["name"]
+
+
+def test_xxh32_stateful_chunkings(manifest):
+    (g,) = cases_of(manifest, "xxh32_stateful")
+    base = O.generate(g["input"]["gen"], g["input"]["seed"], g["input"]["n"])
+    for n, chunk, seed, h in g["rows"]:
+        chunks = [base[p:min(n, p + chunk)] for p in range(0, n, chunk)]
+        assert "%08x" % O.xxh32_stateful(chunks, seed) == h, (n, chunk)
+    seed, n, h = g["empty_updates"]
+    assert "%08x" % O.xxh32_stateful([base[:0], base[:5], base[:0], base[5:n]], seed) == h

@@ -227,6 +227,82 @@ for (const [name, src, genSpec] of blockInputs) {
     manifest.cases.push({ kind: 'digest_4mib', rows });
 }
 
+// ---- 7. compressRaw argument/overflow edge cases (F7, RangeError of output.set) ----
+{
+    const { LZ4Encoder } = await import(path.join(REF, 'src/shared/lz4Encode.js'));
+    const { LZ4Decoder } = await import(path.join(REF, 'src/shared/lz4Decode.js'));
+    const rawCases = [];
+    const rc = (name, src, outLen, start, len, outOff, fiveArgs = false) => {
+        const out = new Uint8Array(outLen);
+        const table = new Int32Array(16384);
+        let r;
+        try {
+            const v = fiveArgs ? compressBlock(src, out, start, len, table) : compressBlock(src, out, start, len, table, outOff);
+            r = { ok: true, value: v };
+        } catch (e) { r = { ok: false, error_name: e.name, error: String(e.message) }; }
+        rawCases.push({ name, src_file: save(src, 'raw_' + name + '_src'), out_len: outLen, start, len, out_off: fiveArgs ? null : outOff,
+            five_args: fiveArgs, ok: r.ok, value: r.ok ? r.value : null, error_name: r.ok ? null : r.error_name, error: r.ok ? null : r.error,
+            out_file: save(out, 'raw_' + name + '_out'), table_file: save(table, 'raw_' + name + '_table') });
+    };
+    const tiles = gen('tiles216', 31, 20000);
+    rc('five_args', tiles, 30000, 0, 20000, 0, true);                 // returns (dIndex - undefined) | 0 == 0
+    rc('five_args_start', tiles, 30000, 1000, 9000, 0, true);
+    const rnd = gen('random', 32, 3000);
+    rc('final_lits_overflow', rnd, 1000, 0, 3000, 0);                  // output.set at :198 throws
+    rc('final_lits_fit', rnd, 3100, 0, 3000, 0);
+    const mixed = new Uint8Array(4000); mixed.set(gen('random', 33, 300), 0); for (let i = 300; i < 4000; i++) mixed[i] = mixed[i - 300];
+    rc('mid_lits_overflow', mixed, 200, 0, 4000, 0);                   // output.set at :100 throws
+    rc('mid_lits_overflow_off', mixed, 400, 0, 4000, 150);
+    rc('short_lits_dropped', new TextEncoder().encode('A'.repeat(10000)), 20, 0, 10000, 0);  // byte stores past the end are dropped
+    manifest.cases.push({ kind: 'compress_raw_edges', cases: rawCases });
+
+    // ---- 8. class XXHash32 over chunked input ------------------------------------
+    const base = gen('random', 41, 70000);
+    const rows = [];
+    for (const n of [0, 1, 15, 16, 17, 31, 32, 33, 100, 4096, 65537, 70000])
+        for (const chunk of [1, 3, 15, 16, 17, 64, 1000, 1 << 20]) {
+            if (n > 5000 && chunk < 15) continue;
+            const st = new XXHash32(n % 2 ? 0x9E3779B1 : 0);
+            for (let p = 0; p < n; p += chunk) st.update(base.subarray(p, Math.min(n, p + chunk)));
+            rows.push([n, chunk, n % 2 ? 0x9E3779B1 : 0, hex(st.digest())]);
+        }
+    const st0 = new XXHash32(7); st0.update(new Uint8Array(0)); st0.update(base.subarray(0, 5)); st0.update(new Uint8Array(0)); st0.update(base.subarray(5, 40));
+    manifest.cases.push({ kind: 'xxh32_stateful', input: { gen: 'random', seed: 41, n: 70000 }, rows,
+        empty_updates: [7, 40, hex(st0.digest())] });
+
+    // ---- 9. LZ4Encoder / LZ4Decoder streams (src/shared/lz4Encode.js, lz4Decode.js) --
+    const streams = [];
+    const sinputs = [['text', gen('text', 51, 300000)], ['tiles216', gen('tiles216', 52, 600000)], ['random', gen('random', 53, 200000)],
+        ['repetitive', gen('repetitive', 54, 150000)], ['random600k', gen('random', 55, 600000)]];
+    for (const [iname, input] of sinputs) for (const bsz of [65536, 262144]) for (const indep of [true, false]) for (const cs of [false, true])
+        for (const chunk of [100000, 65536, 7777]) {
+            if (chunk === 7777 && !(bsz === 65536 && cs)) continue;
+            if (iname === 'random600k' && (bsz !== 262144 || chunk !== 100000)) continue;
+            const enc = new LZ4Encoder(bsz, indep, cs);
+            const parts = [];
+            let err = null;
+            try {
+                for (let p = 0; p < input.length; p += chunk) for (const x of enc.add(input.subarray(p, Math.min(input.length, p + chunk)))) parts.push(x.slice());
+                for (const x of enc.finish()) parts.push(x.slice());
+            } catch (e) { err = e.name + ': ' + e.message; }
+            const lens = parts.map((x) => x.length);
+            const total = lens.reduce((a, b) => a + b, 0);
+            const all = new Uint8Array(total); let o = 0; for (const x of parts) { all.set(x, o); o += x.length; }
+            let dec = null;
+            if (!err) {
+                const d = new LZ4Decoder(null, true);
+                const outs = [];
+                try { for (let p = 0; p < all.length; p += 50000) for (const x of d.update(all.subarray(p, Math.min(all.length, p + 50000)))) outs.push(x); dec = { ok: true, chunks: outs.length, len: outs.reduce((a, b) => a + b.length, 0) }; }
+                catch (e) { dec = { ok: false, error: e.name + ': ' + e.message }; }
+                const f = tryCall(() => decompressBuffer(all));
+                dec.frame_ok = f.ok; dec.frame_equals_input = f.ok && f.value.length === input.length && f.value.every((v, i) => v === input[i]);
+            }
+            streams.push({ input: iname, n: input.length, block: bsz, indep, checksum: cs, chunk, error: err, part_lens: lens,
+                stream_len: total, stream_xxh: err ? null : hex(xxHash32(all)), decoder: dec });
+        }
+    manifest.cases.push({ kind: 'streams', streams });
+}
+
 fs.writeFileSync(path.join(OUT, 'manifest.json'), JSON.stringify(manifest, null, 1));
 console.log('wrote', manifest.cases.length, 'case groups to', OUT);
 }
