@@ -12,10 +12,15 @@ clustered random/tiles216 mix (first half of all ranks' blocks random) dealt
 to the ranks interleaved.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--gen tiles216|random|repetitive|mix|mixc]
+
+With --gpus N > 1 and no torch.distributed environment, the script starts N
+rank processes itself (torch.distributed.run, one per GPU, before touching the
+GPU) and exits with their status; it fails if fewer than N GPUs are visible.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -37,9 +42,28 @@ def parse():
     ap.add_argument("--compress-steps", type=int, default=2)
     ap.add_argument("--extra", type=int, default=1, help="also time the random/repetitive/mix variants")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-blocks", type=int, default=64, help="4 MiB blocks per CPU thread (pure-JS baseline)")
+    ap.add_argument("--napi", type=int, default=1, help="time the JS drop-in end to end (host buffers)")
     ap.add_argument("--frame-steps", type=int, default=3, help="time frame assembly (records + gather to rank 0)")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """--gpus N without a distributed environment: one process per GPU via
+    torch.distributed.run (started before this process touches the GPU)."""
+    import socket
+    import torch
+    have = torch.cuda.device_count()          # does not initialise the GPU on this image
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 class Batch:
@@ -164,15 +188,41 @@ def frame_assembly(torch, dist, lz4mi, batch, stream, stream_obj, steps, world):
     ok = True
     if got[0] is not None:
         ok = bool(torch.equal(got[0][:4], records[:4])) and got[0].numel() == int(tot.item())
-    return {"GBps": round(world * batch.n * BLOCK * steps / wall / 1e9, 2),
-            "ms_per_step": round(wall / steps * 1e3, 3), "frame_bytes": int(tot.item()),
+    return {"record_GBps": round(int(tot.item()) * steps / wall / 1e9, 2),
+            "note": "frame record bytes (size words + payloads) packed and gathered per second",
+            "ms_per_step": round(wall / steps * 1e3, 3), "record_bytes": int(tot.item()),
             "collective": "all_gather(sizes) + send/irecv to rank 0" if dist is not None else None,
             "consistent": ok}
 
 
-def cpu_baseline(lz4mi, batch, torch, threads, target_s=1.5):
-    """The oracle (CPU restatement of the reference decoder) on host cores,
-    over a bounded sample of the same compressed blocks."""
+def cpu_threads():
+    """The host cores this job may use: the box exports OMP_NUM_THREADS (its CPU share)."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(n)) if n and n.isdigit() else (os.cpu_count() or 1)
+
+
+def js_cpu_baseline(gen, blocks):
+    """The pure-JS path (oracle/lz4_js.mjs: our restatement of the reference's
+    compressBlock/decompressBlock, checked against the reference's digests first) on
+    worker_threads over the host's cores, `blocks` distinct 4 MiB blocks per thread."""
+    threads = cpu_threads()
+    r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "oracle", "js_cpu_baseline.mjs"), gen,
+                        str(threads), str(blocks), os.path.join(ROOT, "tests", "golden", "manifest.json")],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": d["decompress_GBps"], "unit": "GB/s", "cores": threads, "kind": "port",
+            "compress_GBps": d["compress_GBps"], "roundtrip_GBps": d["roundtrip_GBps"],
+            "sample": f"pure-JS block codec (oracle/lz4_js.mjs, restatement of blockCompress.js/blockDecompress.js, "
+                      f"bit-exact on {d['golden_digests_checked']} reference 4 MiB digests), {threads} worker_threads "
+                      f"x {blocks} distinct 4 MiB {gen} blocks each, compress then decompress; node {d['node']}, "
+                      f"{d['cpu_model']}; verified={d['verified']}"}
+
+
+def c_cpu_baseline(batch, threads, target_s=1.5):
+    """The C oracle decoder (restatement of blockDecompress.js) on host cores over a
+    bounded sample of the same compressed blocks (second baseline key)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
@@ -193,12 +243,45 @@ def cpu_baseline(lz4mi, batch, torch, threads, target_s=1.5):
     assert (st == 0).all()
     gbps = reps * nb * BLOCK / el / 1e9
     return {"value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"oracle C decoder (restatement of blockDecompress.js), {nb} x 4 MiB blocks of the same "
-                      f"compressed batch, {reps} passes, {threads} pthreads, {el:.1f} s wall"}
+            "sample": f"oracle C decoder, {nb} x 4 MiB blocks of the same compressed batch, {reps} passes, "
+                      f"{threads} pthreads, {el:.1f} s wall"}
+
+
+def napi_e2e(batch, nblocks=64):
+    """LZ4.compress/decompress of the JS drop-in on host buffers (N-API -> liblz4mi), on
+    the first `nblocks` generated blocks: PCIe-inclusive, reported beside the bench."""
+    import tempfile
+    path = os.path.join(tempfile.gettempdir(), f"lz4mi_napi_{os.getpid()}.bin")
+    try:
+        batch.raw[:nblocks * BLOCK].cpu().numpy().tofile(path)
+        r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "tools", "napi_e2e.mjs"), path, "3"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr[-500:]}
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+
+
+def pmc_traffic(lz4mi, n, gen):
+    """HBM bytes per decode launch from the committed rocprofv3 PMC passes, used only when
+    they were measured on this exact build and workload (else null)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if pm.get("workload_blocks") == n and pm.get("generator") == gen and pm.get("build_id") == lz4mi.build_id():
+        return pm.get("hbm_bytes_per_launch"), pm.get("source")
+    return None, None
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args)
     import torch
     import lz4mi
 
@@ -242,6 +325,9 @@ def main():
     ms_per_step = d_wall / args.steps * 1e3
     value = world * raw_bytes * args.steps / d_wall / 1e9
 
+    napi = napi_e2e(batch) if args.napi and rank == 0 and world == 1 else None
+    c_base = c_cpu_baseline(batch, cpu_threads()) if args.cpu_baseline and rank == 0 and world == 1 else None
+
     extra = {}
     if args.extra and rank == 0 and world == 1:
         del batch.dec
@@ -256,12 +342,15 @@ def main():
             extra[g] = {"blocks": nb, "ratio": round(nb * BLOCK / cb, 3),
                         "decompress_GBps": round(nb * BLOCK / k / 1e9, 1),
                         "decompress_hbm_frac": round((nb * BLOCK + cb) / k / 1e9 / HBM_PEAK_GBPS, 4),
-                        "compress_GBps": round(nb * BLOCK / ck / 1e9, 2), "verified": b2.verify(torch, lz4mi, stream)}
+                        "compress_GBps": round(nb * BLOCK / ck / 1e9, 2),
+                        "roundtrip_GBps": round(nb * BLOCK / (ck + k) / 1e9, 2),
+                        "verified": b2.verify(torch, lz4mi, stream)}
             del b2
             torch.cuda.empty_cache()
         batch.dec = torch.empty(1, dtype=torch.uint8, device="cuda")
 
     achieved = (raw_bytes + comp_bytes) / d_kern / 1e9
+    traffic, traffic_src = pmc_traffic(lz4mi, n, args.gen)
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -281,32 +370,30 @@ def main():
                    "compression_ratio": round(raw_bytes / comp_bytes, 3), "parallelism": f"blocks sharded x{world}"},
         "verified": okt.item() == 0,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": "lz4mi_decompress_kernel", "kernel_ms": round(d_kern * 1e3, 3),
                      "algorithmic_bytes_per_launch": raw_bytes + comp_bytes},
         "value_is": "decompress GB/s of uncompressed bytes (the north-star target); compress and the "
-                    "round trip are reported under 'compress' and 'roundtrip_GBps'",
+                    "round trip (compress then decompress of the same bytes) are under 'compress' and "
+                    "'roundtrip_GBps'",
         "compress": {"GBps": round(world * raw_bytes / c_wall * args.compress_steps / 1e9, 2),
                      "kernel_ms": round(c_kern * 1e3, 3),
                      "hbm_frac": round((raw_bytes + comp_bytes) / c_kern / 1e9 / HBM_PEAK_GBPS, 4)},
         "roundtrip_GBps": round(world * raw_bytes / (c_wall / args.compress_steps + d_wall / args.steps) / 1e9, 2),
+        "build_id": lz4mi.build_id(),
     }
-    traffic = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic):
-        try:
-            with open(traffic) as f:
-                pm = json.load(f)
-            if pm.get("workload_blocks") == n and pm.get("generator") == args.gen:
-                line["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-                line["roofline"]["traffic_source"] = pm.get("source")
-        except Exception:
-            pass
+    if traffic_src:
+        line["roofline"]["traffic_source"] = traffic_src
     if frame is not None:
         line["frame"] = frame
     if extra:
         line["variants"] = extra
+    if napi is not None:
+        line["napi_end_to_end"] = napi
     if args.cpu_baseline and rank == 0 and world == 1:
-        line["cpu_baseline"] = cpu_baseline(lz4mi, batch, torch, args.cpu_threads)
+        line["cpu_baseline"] = js_cpu_baseline(args.gen if args.gen in ("tiles216", "random", "repetitive")
+                                               else "tiles216", args.cpu_blocks)
+        line["cpu_baseline_c_oracle"] = c_base
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

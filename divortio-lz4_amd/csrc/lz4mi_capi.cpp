@@ -1,18 +1,25 @@
 // lz4mi_capi.cpp — host side of liblz4mi.so: the C-ABI declared in
-// include/lz4mi.h. Owns the per-device context (stream, grow-only device
-// scratch), stages host buffers for the synchronous entry points and launches
-// the gfx950 kernels. No CPU fallback: without a gfx950 device every entry
-// point that needs the GPU returns LZ4MI_ERR_NO_DEVICE.
+// include/lz4mi.h. Owns the per-device context (library stream, staging buffers
+// of the synchronous host-pointer entry points) and one scratch set per HIP
+// stream for the asynchronous device-pointer entry points, and launches the
+// gfx950 kernels. No CPU fallback: without a gfx950 device every entry point
+// that needs the GPU returns LZ4MI_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <vector>
 
 #include "../../include/lz4mi.h"
+#include "lz4mi_decompress.h"
+
+#ifndef LZ4MI_SRC_HASH
+#define LZ4MI_SRC_HASH "unknown"
+#endif
 
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
@@ -21,52 +28,71 @@ extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t*, const uint
                                                       const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
                                                       uint32_t*, int32_t*, uint32_t, const uint64_t*, const uint32_t*,
                                                       hipStream_t);
-extern "C" hipError_t lz4mi_launch_token_map(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
-                                             uint32_t, const uint32_t*, uint64_t*, uint32_t, uint32_t, hipStream_t);
-extern "C" hipError_t lz4mi_launch_ring_decode(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
-                                               const uint64_t*, const uint32_t*, uint32_t*, int32_t*, const uint32_t*,
-                                               const uint64_t*, uint32_t, uint32_t*, uint32_t, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
                                               const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*, uint32_t,
-                                              hipStream_t);
+                                              uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int32_t, int32_t, int32_t*, uint8_t*,
                                                   uint64_t, int32_t, int64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
-                                         uint32_t, int, hipStream_t);
+                                         uint32_t, int, uint8_t*, const uint64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_generate(uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 
 namespace {
 
+// Grow-only device buffer. Work using the old buffer may still be queued on
+// `s` (the only stream that uses it), so the old one is freed stream-ordered.
 struct Scratch {
     void* p = nullptr;
     size_t cap = 0;
-    hipError_t ensure(size_t n) {
+    hipError_t ensure(size_t n, hipStream_t s) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, s);
         p = nullptr;
         cap = 0;
-        size_t want = std::max<size_t>(n, 1 << 20);
+        size_t want = std::max<size_t>(n + n / 4, 1 << 20);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
     }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Scratch of the work enqueued on one stream: kernels on one stream run in
+// order, so reusing it needs no lock or event; different streams never share.
+struct StreamCtx {
+    hipStream_t stream = nullptr;
+    Scratch tables;       // batch encoder hash tables (64 KiB per block)
+    Scratch chunk_base;   // two-pass decoder: first bitmap chunk of each block (device plan)
+    Scratch bitmap;       // token bitmaps, 128 B per 1 KiB compressed chunk
+    Scratch frame_meta;   // block-checksum payload offsets / lengths of frame_pack
+    uint64_t bitmap_chunks = 0;
+    uint32_t* needed = nullptr;   // host-mapped: chunks the last plan wanted (read lazily)
+    void release() {
+        tables.release();
+        chunk_base.release();
+        bitmap.release();
+        frame_meta.release();
+        if (needed) (void)hipHostFree(needed);
+        needed = nullptr;
+        bitmap_chunks = 0;
+    }
 };
 
 struct Ctx {
     int device = -1;
     hipStream_t stream = nullptr;
-    Scratch in, out, meta, aux;
-    Scratch tables;   // batch encoder hash tables (64 KiB per block)
-    // two-pass decoder: per-block chunk index, token bitmaps (128 B per 1 KiB chunk), counters
-    Scratch chunk_base, bitmap, stats;
-    std::vector<uint32_t> h_len, h_base;
-    uint32_t* h_pin = nullptr;   // pinned staging for the block lengths of device-pointer calls
-    size_t h_pin_cap = 0;
-    hipEvent_t ring_done = nullptr;   // the two-pass scratch is free once this has fired
-    std::mutex mu, ring_mu;
+    Scratch in, out, meta, aux;   // staging of the synchronous host-pointer entry points
+    std::mutex mu;                // serialises the host-pointer entry points (their staging is shared)
+    std::mutex streams_mu;
+    std::vector<std::unique_ptr<StreamCtx>> streams;
+    Scratch stats;
 };
 
 Ctx g_ctx;
@@ -79,13 +105,25 @@ std::mutex g_init_mu;
     } while (0)
 
 int32_t ensure_init() {
-    if (g_ctx.device >= 0) return LZ4MI_OK;
+    if (g_ctx.device >= 0) {
+        // HIP's current device is per host thread: callers may come from any thread
+        return hipSetDevice(g_ctx.device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
+    }
     return lz4mi_init(-1);
 }
 
 hipStream_t pick_stream(void* s) { return s ? static_cast<hipStream_t>(s) : g_ctx.stream; }
 
-constexpr uint32_t kRingChunk = 1024;   // lz4mi_decompress_ring.hip kC
+StreamCtx* stream_ctx(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_ctx.streams_mu);
+    for (auto& c : g_ctx.streams)
+        if (c->stream == s) return c.get();
+    g_ctx.streams.emplace_back(new StreamCtx());
+    g_ctx.streams.back()->stream = s;
+    return g_ctx.streams.back().get();
+}
+
+constexpr uint64_t kBitmapChunks0 = 1u << 19;   // initial bitmap capacity: 512 Ki chunks = 64 MiB
 
 // Decoder selection (LZ4MI_DECODER): "auto" (default) = the two-pass ring decoder for
 // blocks compressed at least kRingRatio:1 (long matches: it writes them from LDS), the
@@ -103,87 +141,110 @@ bool ring_enabled() {
     return g_ring_mode == 1;
 }
 
-// Spec-mode decode of a batch whose pointers are all device pointers: the
-// two-pass ring decoder, then the single-pass kernel for the blocks it hands
-// back. h_in_len: the block lengths if the caller has them on the host (else
-// they are read back from the device, one small synchronous copy).
-hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* h_in_len,
-                       uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
-                       uint32_t dict_len, uint32_t* out_len, int32_t* status, uint32_t nblocks, hipStream_t s) {
-    std::lock_guard<std::mutex> lk(g_ctx.ring_mu);
+// Spec-mode decode of a batch whose pointers are all device pointers: a
+// device-side plan (which blocks the two-pass ring decoder takes, their bitmap
+// chunks), pass 1 + pass 2 of the ring decoder, then the single-pass kernel for
+// every other block. Nothing is read back: the call only enqueues. The bitmap
+// scratch is sized from what earlier plans on this stream needed (a host-mapped
+// word the plan writes); blocks that do not fit this call's scratch simply go to
+// the single-pass kernel.
+hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                       const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
+                       uint32_t* out_len, int32_t* status, uint32_t nblocks, hipStream_t s) {
+    StreamCtx* c = stream_ctx(s);
     hipError_t e;
-    if (!g_ctx.ring_done) {
-        if ((e = hipEventCreateWithFlags(&g_ctx.ring_done, hipEventDisableTiming)) != hipSuccess) return e;
-    } else if ((e = hipStreamWaitEvent(s, g_ctx.ring_done, 0)) != hipSuccess) {
-        return e;
+    if (!c->needed) {
+        if ((e = hipHostMalloc((void**)&c->needed, 64, hipHostMallocMapped)) != hipSuccess) return e;
+        *c->needed = 0;
     }
-    const uint32_t* lens = h_in_len;
-    if (!lens) {
-        if (g_ctx.h_pin_cap < nblocks) {
-            if (g_ctx.h_pin) (void)hipHostFree(g_ctx.h_pin);
-            g_ctx.h_pin = nullptr;
-            g_ctx.h_pin_cap = 0;
-            if ((e = hipHostMalloc((void**)&g_ctx.h_pin, 4ull * nblocks, 0)) != hipSuccess) return e;
-            g_ctx.h_pin_cap = nblocks;
-        }
-        if ((e = hipMemcpyAsync(g_ctx.h_pin, in_len, 4ull * nblocks, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        lens = g_ctx.h_pin;
+    uint64_t want = std::max<uint64_t>(kBitmapChunks0, (uint64_t)*c->needed);
+    uint64_t limit = UINT64_MAX;
+    if (const char* cap = std::getenv("LZ4MI_RING_MAX_CHUNKS")) {   // tests: a small scratch forces overflow
+        limit = std::strtoull(cap, nullptr, 10);
+        want = limit;
     }
-    g_ctx.h_base.resize(nblocks);
-    uint64_t total = 0;
-    uint32_t maxc = 0;
-    for (uint32_t b = 0; b < nblocks; ++b) {
-        const uint32_t c = (lens[b] + kRingChunk - 1) / kRingChunk;
-        g_ctx.h_base[b] = (uint32_t)total;
-        total += c;
-        maxc = std::max(maxc, c);
+    if (want > c->bitmap_chunks) {
+        if ((e = c->bitmap.ensure(want * 128 + 64, s)) != hipSuccess) return e;
+        c->bitmap_chunks = (c->bitmap.cap - 64) / 128;
     }
-    if (total >= 0xFFFFFFFFull) return hipErrorInvalidValue;
-    if ((e = g_ctx.chunk_base.ensure(4ull * nblocks + 64)) != hipSuccess) return e;
-    if ((e = g_ctx.bitmap.ensure(128ull * total + 64)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(g_ctx.chunk_base.p, g_ctx.h_base.data(), 4ull * nblocks, hipMemcpyHostToDevice, s)) !=
-        hipSuccess)
-        return e;
+    const uint64_t capacity = std::min<uint64_t>(c->bitmap_chunks, limit);
+    if ((e = c->chunk_base.ensure(4ull * nblocks + 64, s)) != hipSuccess) return e;
+    uint32_t* needed_dev = nullptr;
+    if ((e = hipHostGetDevicePointer((void**)&needed_dev, c->needed, 0)) != hipSuccess) return e;
     uint32_t* stats = nullptr;
     if (std::getenv("LZ4MI_RING_STATS")) {
         if (!g_ctx.stats.p) {
-            if ((e = g_ctx.stats.ensure(64)) != hipSuccess) return e;
+            if ((e = g_ctx.stats.ensure(64, s)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(g_ctx.stats.p, 0, 64, s)) != hipSuccess) return e;
         }
         stats = g_ctx.stats.as<uint32_t>();
     }
-    // LZ4MI_BITMAP=1: pass 1 maps every block and the single-pass kernel takes its token starts from it
-    static const bool bm_mode = std::getenv("LZ4MI_BITMAP") && std::getenv("LZ4MI_BITMAP")[0] == '1';
-    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, bm_mode ? 0u : g_ring_ratio, g_ctx.chunk_base.as<uint32_t>(),
-                                    g_ctx.bitmap.as<uint64_t>(), nblocks, maxc, s)) != hipSuccess)
+    if ((e = lz4mi_launch_ring_plan(in_len, out_cap, g_ring_ratio, nblocks, capacity,
+                                    c->chunk_base.as<uint32_t>(), needed_dev, s)) != hipSuccess)
+        return e;
+    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, g_ring_ratio, c->chunk_base.as<uint32_t>(),
+                                    c->bitmap.as<uint64_t>(), nblocks, s)) != hipSuccess)
         return e;
     if ((e = lz4mi_launch_ring_decode(in, in_off, in_len, out, out_off, out_cap, out_len, status,
-                                      g_ctx.chunk_base.as<uint32_t>(), g_ctx.bitmap.as<uint64_t>(), g_ring_ratio, stats,
+                                      c->chunk_base.as<uint32_t>(), c->bitmap.as<uint64_t>(), g_ring_ratio, stats,
                                       nblocks, s)) != hipSuccess)
         return e;
-    if ((e = lz4mi_launch_decompress_pending(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
-                                             status, nblocks, bm_mode ? g_ctx.bitmap.as<uint64_t>() : nullptr,
-                                             g_ctx.chunk_base.as<uint32_t>(), s)) != hipSuccess)
-        return e;
-    return hipEventRecord(g_ctx.ring_done, s);
+    return lz4mi_launch_decompress_pending(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
+                                           nblocks, nullptr, nullptr, s);
 }
 
-hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* h_in_len,
-                         uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
-                         uint32_t dict_len, uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode,
-                         hipStream_t s) {
+hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                         const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
+                         uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s) {
     if (mode == 0 && ring_enabled())
-        return ring_decode(in, in_off, in_len, h_in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
-                           nblocks, s);
+        return ring_decode(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks, s);
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
                                    nblocks, mode, s);
 }
+
+inline uint64_t round16(uint64_t n) { return (n + 15u) & ~15ull; }
 
 // ---- host XXH32 (reference variant by default, see lz4mi_xxh32.hip) -------
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
 inline uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 inline uint32_t le32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+
+inline uint32_t converge(const uint32_t v[4], uint32_t flags) {
+    if (flags & LZ4MI_XXH_STANDARD) return rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18);
+    return rotl(rotl(rotl(rotl(v[0], 1) + v[1], 7) + v[2], 12) + v[3], 18);   // xxhash32.js:59-65
+}
+
+inline uint32_t tail_mix(uint32_t h, const uint8_t* p, size_t n) {
+    size_t k = 0;
+    for (; k + 4 <= n; k += 4) h = rotl(h + le32(p + k) * P3, 17) * P4;
+    for (; k < n; ++k) h = rotl(h + p[k] * P5, 11) * P1;
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+
+inline void stripes(uint32_t v[4], const uint8_t* p, size_t n16) {
+    uint32_t a = v[0], b = v[1], c = v[2], d = v[3];
+    for (size_t k = 0; k < n16; ++k, p += 16) {
+        a = rotl(a + le32(p) * P2, 13) * P1;
+        b = rotl(b + le32(p + 4) * P2, 13) * P1;
+        c = rotl(c + le32(p + 8) * P2, 13) * P1;
+        d = rotl(d + le32(p + 12) * P2, 13) * P1;
+    }
+    v[0] = a; v[1] = b; v[2] = c; v[3] = d;
+}
+
+// Streaming state (include/lz4mi.h lz4mi_xxh32_state): v[4], seed, mem_size,
+// total (u64), mem[16], flags.
+struct XxhState {
+    uint32_t v[4];
+    uint32_t seed;
+    uint32_t mem_size;
+    uint64_t total;
+    uint8_t mem[16];
+    uint32_t flags;
+    uint32_t pad;
+};
+static_assert(sizeof(XxhState) == sizeof(lz4mi_xxh32_state), "lz4mi_xxh32_state layout");
 
 }  // namespace
 
@@ -199,8 +260,9 @@ const char* lz4mi_status_message(int32_t s) {
         case LZ4MI_ERR_MAGIC: return "LZ4: Invalid Magic Number";
         case LZ4MI_ERR_VERSION: return "LZ4: Unsupported Version";
         case LZ4MI_ERR_CHECKSUM: return "LZ4: Content Checksum Error";
-        case LZ4MI_ERR_RANGE: return "offset is out of bounds";
+        case LZ4MI_ERR_RANGE: return "Source is too large";
         case LZ4MI_ERR_CROSS_BLOCK: return "lz4mi: block references data before its start (not an independent block)";
+        case LZ4MI_ERR_BLOCK_CHECKSUM: return "LZ4: Block Checksum Error";
         case LZ4MI_ERR_HIP: return "lz4mi: HIP runtime error";
         case LZ4MI_ERR_ARG: return "lz4mi: invalid argument";
         case LZ4MI_ERR_NO_DEVICE: return "lz4mi: no gfx950 (MI355X) device available";
@@ -229,7 +291,9 @@ int32_t lz4mi_debug_set_decoder(int32_t mode, uint32_t ratio) {
     return LZ4MI_OK;
 }
 
-const char* lz4mi_version(void) { return "lz4mi 0.1 (gfx950)"; }
+const char* lz4mi_version(void) { return "lz4mi 0.2 (gfx950) src " LZ4MI_SRC_HASH; }
+
+const char* lz4mi_build_id(void) { return LZ4MI_SRC_HASH; }
 
 int32_t lz4mi_device_count(void) {
     int n = 0;
@@ -242,44 +306,97 @@ int32_t lz4mi_init(int32_t device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return LZ4MI_ERR_NO_DEVICE;
     if (device < 0) {
+        if (g_ctx.device >= 0) return hipSetDevice(g_ctx.device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
         if (hipGetDevice(&device) != hipSuccess) device = 0;
     }
     if (device >= n) return LZ4MI_ERR_ARG;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return LZ4MI_ERR_HIP;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LZ4MI_ERR_NO_DEVICE;
-    if (g_ctx.device == device) return LZ4MI_OK;
+    if (g_ctx.device == device) return hipSetDevice(device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
+    if (g_ctx.device >= 0) {
+        // switching devices: every buffer of the old context lives on the old device
+        std::lock_guard<std::mutex> lk2(g_ctx.mu);
+        LZ4MI_TRY(hipSetDevice(g_ctx.device));
+        LZ4MI_TRY(hipDeviceSynchronize());
+        g_ctx.in.release();
+        g_ctx.out.release();
+        g_ctx.meta.release();
+        g_ctx.aux.release();
+        g_ctx.stats.release();
+        {
+            std::lock_guard<std::mutex> lk3(g_ctx.streams_mu);
+            for (auto& c : g_ctx.streams) c->release();
+            g_ctx.streams.clear();
+        }
+        if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
+        g_ctx.stream = nullptr;
+        g_ctx.device = -1;
+    }
     LZ4MI_TRY(hipSetDevice(device));
-    if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     LZ4MI_TRY(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     g_ctx.device = device;
     return LZ4MI_OK;
 }
 
 uint32_t lz4mi_xxh32(const uint8_t* in, size_t len, uint32_t seed, uint32_t flags) {
-    size_t p = 0;
     uint32_t h;
+    const size_t n16 = len / 16;
     if (len >= 16) {
-        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
-        for (; p + 16 <= len; p += 16) {
-            v1 = rotl(v1 + le32(in + p) * P2, 13) * P1;
-            v2 = rotl(v2 + le32(in + p + 4) * P2, 13) * P1;
-            v3 = rotl(v3 + le32(in + p + 8) * P2, 13) * P1;
-            v4 = rotl(v4 + le32(in + p + 12) * P2, 13) * P1;
-        }
-        if (flags & LZ4MI_XXH_STANDARD) {
-            h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
-        } else {   // the reference's chained convergence (xxhash32.js:59-65)
-            h = rotl(rotl(rotl(rotl(v1, 1) + v2, 7) + v3, 12) + v4, 18);
-        }
+        uint32_t v[4] = {seed + P1 + P2, seed + P2, seed, seed - P1};
+        stripes(v, in, n16);
+        h = converge(v, flags);
     } else {
         h = seed + P5;
     }
     h += (uint32_t)len;
-    for (; p + 4 <= len; p += 4) h = rotl(h + le32(in + p) * P3, 17) * P4;
-    for (; p < len; ++p) h = rotl(h + in[p] * P5, 11) * P1;
-    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
-    return h;
+    const size_t p = len >= 16 ? n16 * 16 : 0;
+    return tail_mix(h, in + p, len - p);
+}
+
+void lz4mi_xxh32_reset(lz4mi_xxh32_state* st, uint32_t seed, uint32_t flags) {
+    XxhState* s = reinterpret_cast<XxhState*>(st);
+    std::memset(s, 0, sizeof *s);
+    s->v[0] = seed + P1 + P2;
+    s->v[1] = seed + P2;
+    s->v[2] = seed;
+    s->v[3] = seed - P1;
+    s->seed = seed;
+    s->flags = flags;
+}
+
+void lz4mi_xxh32_update(lz4mi_xxh32_state* st, const uint8_t* in, size_t len) {
+    XxhState* s = reinterpret_cast<XxhState*>(st);
+    s->total += len;
+    if (s->mem_size + len < 16) {                       // xxhash32Stateful.js:40-44
+        if (len) std::memcpy(s->mem + s->mem_size, in, len);
+        s->mem_size += (uint32_t)len;
+        return;
+    }
+    size_t p = 0;
+    if (s->mem_size > 0) {                              // :46-54
+        p = 16 - s->mem_size;
+        std::memcpy(s->mem + s->mem_size, in, p);
+        stripes(s->v, s->mem, 1);
+        s->mem_size = 0;
+    }
+    const size_t n16 = (len - p) / 16;                  // :57-61
+    stripes(s->v, in + p, n16);
+    p += n16 * 16;
+    if (p < len) {                                      // :64-67
+        std::memcpy(s->mem, in + p, len - p);
+        s->mem_size = (uint32_t)(len - p);
+    }
+}
+
+uint32_t lz4mi_xxh32_digest(const lz4mi_xxh32_state* st) {
+    const XxhState* s = reinterpret_cast<const XxhState*>(st);
+    // the class keeps totalLen as `(totalLen + len) | 0` (:37) and tests it signed (:113);
+    // LZ4MI_XXH_LEN64 keeps the full length (streams over 2 GiB)
+    const bool big = (s->flags & LZ4MI_XXH_LEN64) ? s->total >= 16 : (int32_t)(uint32_t)s->total >= 16;
+    uint32_t h = big ? converge(s->v, s->flags) : s->seed + P5;
+    h += (uint32_t)s->total;
+    return tail_mix(h, s->mem, s->mem_size);
 }
 
 int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
@@ -292,11 +409,13 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
-        LZ4MI_TRY(decode_launch(in, in_off, in_len, nullptr, out, out_off, out_cap, dict, dict_len, out_len, status,
-                                nblocks, mode, pick_stream(stream)));
+        LZ4MI_TRY(decode_launch(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
+                                mode, pick_stream(stream)));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_cap || !out_len || !status) return LZ4MI_ERR_ARG;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        if (in_len[b] > LZ4MI_MAX_BLOCK || out_cap[b] > LZ4MI_MAX_BLOCK) return LZ4MI_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     hipStream_t s = g_ctx.stream;
     // Pack the compressed blocks; stage the output image [lo - hist, hi) so
@@ -304,7 +423,7 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     // positions are absolute in `out`) see the caller's bytes.
     uint64_t in_total = 0, lo = UINT64_MAX, hi = 0;
     for (uint32_t b = 0; b < nblocks; ++b) {
-        in_total += (in_len[b] + 15u) & ~15ull;
+        in_total += round16(in_len[b]);
         lo = std::min<uint64_t>(lo, out_off[b]);
         hi = std::max<uint64_t>(hi, out_off[b] + out_cap[b]);
     }
@@ -314,16 +433,16 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     uint64_t pos = 0;
     for (uint32_t b = 0; b < nblocks; ++b) {
         d_in_off[b] = pos;
-        pos += (in_len[b] + 15u) & ~15ull;
+        pos += round16(in_len[b]);
         d_out_off[b] = out_off[b] - base;
     }
     // Dictionary bytes are only reachable when the image starts at out[0].
     uint32_t dlen = (base == 0 && dict) ? dict_len : 0;
-    LZ4MI_TRY(g_ctx.in.ensure(in_total + 64));
-    LZ4MI_TRY(g_ctx.out.ensure(img + 64));
-    LZ4MI_TRY(g_ctx.aux.ensure((size_t)dlen + 64));
+    LZ4MI_TRY(g_ctx.in.ensure(in_total + 64, s));
+    LZ4MI_TRY(g_ctx.out.ensure(img + 64, s));
+    LZ4MI_TRY(g_ctx.aux.ensure((size_t)dlen + 64, s));
     const size_t meta_bytes = (size_t)nblocks * (8 + 4 + 8 + 4 + 4 + 4);
-    LZ4MI_TRY(g_ctx.meta.ensure(meta_bytes + 64));
+    LZ4MI_TRY(g_ctx.meta.ensure(meta_bytes + 64, s));
     uint8_t* m = g_ctx.meta.as<uint8_t>();
     uint64_t* m_in_off = (uint64_t*)m;
     uint64_t* m_out_off = m_in_off + nblocks;
@@ -343,9 +462,8 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, in_len, g_ctx.out.as<uint8_t>(), m_out_off,
-                            m_out_cap, dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks,
-                            mode, s));
+    LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off, m_out_cap,
+                            dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks, mode, s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
@@ -375,28 +493,29 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
     if (st) return st;
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
-        // the table scratch is the context's: launches through it are serialised on the context's lock
-        // and ordered on one stream per context use (see include/lz4mi.h)
-        std::lock_guard<std::mutex> lk(g_ctx.mu);
-        LZ4MI_TRY(g_ctx.tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t)));
-        LZ4MI_TRY(lz4mi_launch_compress(in, in_off, in_len, out, out_off, out_len, nblocks, g_ctx.tables.as<int32_t>(),
-                                        pick_stream(stream)));
+        // the hash-table scratch belongs to the stream: kernels of one stream use it in order
+        hipStream_t s = pick_stream(stream);
+        StreamCtx* c = stream_ctx(s);
+        LZ4MI_TRY(c->tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t), s));
+        LZ4MI_TRY(lz4mi_launch_compress(in, in_off, in_len, out, out_off, out_len, nblocks, c->tables.as<int32_t>(), s));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_len) return LZ4MI_ERR_ARG;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        if (in_len[b] > LZ4MI_MAX_BLOCK) return LZ4MI_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     hipStream_t s = g_ctx.stream;
     std::vector<uint64_t> d_in_off(nblocks), d_out_off(nblocks);
     uint64_t ipos = 0, opos = 0;
     for (uint32_t b = 0; b < nblocks; ++b) {
         d_in_off[b] = ipos;
-        ipos += (in_len[b] + 15u) & ~15ull;
+        ipos += round16(in_len[b]);
         d_out_off[b] = opos;
-        opos += (lz4mi_compress_bound(in_len[b]) + 15u) & ~15ull;
+        opos += round16(lz4mi_compress_bound(in_len[b]));
     }
-    LZ4MI_TRY(g_ctx.in.ensure(ipos + 64));
-    LZ4MI_TRY(g_ctx.out.ensure(opos + 64));
-    LZ4MI_TRY(g_ctx.meta.ensure((size_t)nblocks * 24 + 64));
+    LZ4MI_TRY(g_ctx.in.ensure(ipos + 64, s));
+    LZ4MI_TRY(g_ctx.out.ensure(opos + 64, s));
+    LZ4MI_TRY(g_ctx.meta.ensure((size_t)nblocks * 24 + 64, s));
     uint64_t* m_in_off = g_ctx.meta.as<uint64_t>();
     uint64_t* m_out_off = m_in_off + nblocks;
     uint32_t* m_in_len = (uint32_t*)(m_out_off + nblocks);
@@ -407,9 +526,10 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
     LZ4MI_TRY(hipMemcpyAsync(m_in_off, d_in_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(g_ctx.tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t)));
+    StreamCtx* c = stream_ctx(s);
+    LZ4MI_TRY(c->tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t), s));
     LZ4MI_TRY(lz4mi_launch_compress(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off,
-                                    m_out_len, nblocks, g_ctx.tables.as<int32_t>(), s));
+                                    m_out_len, nblocks, c->tables.as<int32_t>(), s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
     for (uint32_t b = 0; b < nblocks; ++b)
@@ -427,6 +547,7 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
     if (st) return st;
     if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table)
         return LZ4MI_ERR_ARG;
+    if (out_off < 0) return LZ4MI_ERR_ARG;
     if (flags & LZ4MI_DEVICE_PTRS) return LZ4MI_ERR_ARG;   // host-only entry point (see header)
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     hipStream_t s = pick_stream(stream);
@@ -436,9 +557,9 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
     int64_t base = std::max<int64_t>(0, (int64_t)src_start - 65536);
     uint64_t sbytes = (uint64_t)src_start + src_len - base;
     uint64_t obytes = out_total > (uint64_t)out_off ? out_total - (uint64_t)out_off : 0;
-    LZ4MI_TRY(g_ctx.in.ensure(sbytes + 64));
-    LZ4MI_TRY(g_ctx.out.ensure(obytes + 64));
-    LZ4MI_TRY(g_ctx.meta.ensure(16384 * 4 + 64));
+    LZ4MI_TRY(g_ctx.in.ensure(sbytes + 64, s));
+    LZ4MI_TRY(g_ctx.out.ensure(obytes + 64, s));
+    LZ4MI_TRY(g_ctx.meta.ensure(16384 * 4 + 64, s));
     std::vector<int32_t> t(16384);
     for (int k = 0; k < 16384; ++k) t[k] = (int32_t)((uint32_t)table[k] - (uint32_t)base);
     int32_t* d_table = g_ctx.meta.as<int32_t>();
@@ -447,14 +568,17 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
     LZ4MI_TRY(hipMemcpyAsync(d_table, t.data(), 16384 * 4, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(lz4mi_launch_compress_table(g_ctx.in.as<uint8_t>(), sbytes, (int32_t)(src_start - base), src_len,
                                           d_table, g_ctx.out.as<uint8_t>(), obytes, 0, d_ret, s));
-    int64_t ret = 0;
-    LZ4MI_TRY(hipMemcpyAsync(&ret, d_ret, 8, hipMemcpyDeviceToHost, s));
+    int64_t ret[2] = {0, 0};
+    LZ4MI_TRY(hipMemcpyAsync(ret, d_ret, 16, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(t.data(), d_table, 16384 * 4, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
-    uint64_t n = std::min<uint64_t>((uint64_t)ret, obytes);
+    uint64_t n = std::min<uint64_t>((uint64_t)ret[0], obytes);
     if (n) LZ4MI_TRY(hipMemcpy(out + out_off, g_ctx.out.p, n, hipMemcpyDeviceToHost));
     for (int k = 0; k < 16384; ++k) table[k] = (int32_t)((uint32_t)t[k] + (uint32_t)base);
-    return ret;
+    // the reference threw a RangeError from output.set (blockCompress.js:100,198): the bytes and
+    // table entries written before it stay written
+    if (ret[1]) return LZ4MI_ERR_RANGE;
+    return ret[0];
 }
 
 int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
@@ -464,16 +588,17 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
     const int stdv = (flags & LZ4MI_XXH_STANDARD) ? 1 : 0;
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
-        LZ4MI_TRY(lz4mi_launch_xxh32(in, off, len, seed, hashes, nblocks, stdv, pick_stream(stream)));
+        LZ4MI_TRY(lz4mi_launch_xxh32(in, off, len, seed, hashes, nblocks, stdv, nullptr, nullptr, pick_stream(stream)));
         return LZ4MI_OK;
     }
+    if (!in || !off || !len || !hashes) return LZ4MI_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     hipStream_t s = g_ctx.stream;
     std::vector<uint64_t> d_off(nblocks);
     uint64_t pos = 0;
-    for (uint32_t b = 0; b < nblocks; ++b) { d_off[b] = pos; pos += (len[b] + 15u) & ~15ull; }
-    LZ4MI_TRY(g_ctx.in.ensure(pos + 64));
-    LZ4MI_TRY(g_ctx.meta.ensure((size_t)nblocks * 16 + 64));
+    for (uint32_t b = 0; b < nblocks; ++b) { d_off[b] = pos; pos += round16(len[b]); }
+    LZ4MI_TRY(g_ctx.in.ensure(pos + 64, s));
+    LZ4MI_TRY(g_ctx.meta.ensure((size_t)nblocks * 16 + 64, s));
     uint64_t* m_off = g_ctx.meta.as<uint64_t>();
     uint32_t* m_len = (uint32_t*)(m_off + nblocks);
     uint32_t* m_h = m_len + nblocks;
@@ -481,7 +606,7 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
         LZ4MI_TRY(hipMemcpyAsync(g_ctx.in.as<uint8_t>() + d_off[b], in + off[b], len[b], hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_off, d_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_len, len, 4ull * nblocks, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(lz4mi_launch_xxh32(g_ctx.in.as<uint8_t>(), m_off, m_len, seed, m_h, nblocks, stdv, s));
+    LZ4MI_TRY(lz4mi_launch_xxh32(g_ctx.in.as<uint8_t>(), m_off, m_len, seed, m_h, nblocks, stdv, nullptr, nullptr, s));
     LZ4MI_TRY(hipMemcpyAsync(hashes, m_h, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
     return LZ4MI_OK;
@@ -493,8 +618,24 @@ int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint
     int32_t st = ensure_init();
     if (st) return st;
     if (!(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
+    if (nblocks == 0) return LZ4MI_OK;
+    hipStream_t s = pick_stream(stream);
+    if (!(flags & LZ4MI_BLOCK_CHECKSUM)) {
+        LZ4MI_TRY(lz4mi_launch_frame_pack(raw, raw_off, raw_len, comp, comp_off, comp_len, frame, rec_off, nblocks,
+                                          nullptr, nullptr, nullptr, s));
+        return LZ4MI_OK;
+    }
+    // records carry XXH32 (spec) of their payload after it: the pack kernel writes each
+    // payload's position and length, the batched XXH32 kernel hashes the payloads in place
+    // and stores each digest after its payload
+    StreamCtx* c = stream_ctx(s);
+    LZ4MI_TRY(c->frame_meta.ensure((size_t)nblocks * 20 + 64, s));
+    uint64_t* pay_off = c->frame_meta.as<uint64_t>();
+    uint64_t* sum_off = pay_off + nblocks;
+    uint32_t* pay_len = (uint32_t*)(sum_off + nblocks);
     LZ4MI_TRY(lz4mi_launch_frame_pack(raw, raw_off, raw_len, comp, comp_off, comp_len, frame, rec_off, nblocks,
-                                      pick_stream(stream)));
+                                      pay_off, sum_off, pay_len, s));
+    LZ4MI_TRY(lz4mi_launch_xxh32(frame, pay_off, pay_len, 0, nullptr, nblocks, 1, frame, sum_off, s));
     return LZ4MI_OK;
 }
 

@@ -113,8 +113,11 @@ __device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int6
 }
 
 // Token + literal-length extension bytes + literals; returns the new output position.
+// A run of more than 64 literals is one output.set() in the reference (blockCompress.js:100,
+// :198), which throws a RangeError instead of writing when the run does not fit: `range`
+// is set and the position after the length bytes returned (what was written stays).
 __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t anchor, int64_t lit,
-                                 uint32_t mnib) {
+                                 uint32_t mnib, bool& range) {
     uint32_t tok = (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib;
     if (lane == 0) put_byte(j, op, tok);
     ++op;
@@ -125,11 +128,15 @@ __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t
         if (lane == 0) put_byte(j, op + nff, (uint32_t)(ext - 255 * nff));
         op += nff + 1;
     }
+    if (lit > 64 && (uint64_t)(op + lit) > j.dst_total) {
+        range = true;
+        return op;
+    }
     wave_copy(j, lane, op, anchor, lit);
     return op + lit;
 }
 
-__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane) {
+__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range) {
     const int64_t end = (int64_t)j.start + j.len;
     const int64_t mflimit = end - 12;
     const int64_t matchlimit = end - 5;
@@ -195,7 +202,8 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane) {
         }
         int64_t mcode = e - i - 4;
         int64_t lit = i - anchor;
-        op = emit_literals(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode);
+        op = emit_literals(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range);
+        if (range) return op - j.dst_pos;
         uint32_t off = (uint32_t)(i - cand);
         if (lane == 0) { put_byte(j, op, off & 255); put_byte(j, op + 1, (off >> 8) & 255); }
         op += 2;
@@ -209,7 +217,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane) {
         i = e;
         anchor = e;
     }
-    op = emit_literals(j, lane, op, anchor, end - anchor, 0);
+    op = emit_literals(j, lane, op, anchor, end - anchor, 0, range);
     return op - j.dst_pos;
 }
 
@@ -232,13 +240,18 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
     }
     for (int k = lane; k < 16384; k += kWave) T[k] = j.table ? j.table[k] : 0;
     __syncthreads();
-    int64_t n = compress_block_wave(j, T, lane);
+    bool range = false;
+    int64_t n = compress_block_wave(j, T, lane, range);
     __syncthreads();
     if (j.table)
         for (int k = lane; k < 16384; k += kWave) j.table[k] = T[k];
     if (lane == 0) {
-        if (a.nblocks == 0) *a.single_ret = n;
-        else a.out_len[blockIdx.x] = (uint32_t)n;
+        if (a.nblocks == 0) {
+            a.single_ret[0] = n;
+            a.single_ret[1] = range ? 1 : 0;   // RangeError of output.set (the reference throws)
+        } else {
+            a.out_len[blockIdx.x] = (uint32_t)n;
+        }
     }
 }
 

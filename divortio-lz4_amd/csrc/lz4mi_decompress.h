@@ -34,10 +34,12 @@ extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hi
 extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream);
 
 // Two-pass ring decoder (lz4mi_decompress_ring.hip).
+extern "C" hipError_t lz4mi_launch_ring_plan(const uint32_t* in_len, const uint32_t* out_cap, uint32_t min_ratio,
+                                             uint32_t nblocks, uint64_t capacity_chunks, uint32_t* chunk_base,
+                                             uint32_t* needed, hipStream_t stream);
 extern "C" hipError_t lz4mi_launch_token_map(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                              const uint32_t* out_cap, uint32_t min_ratio, const uint32_t* chunk_base,
-                                             uint64_t* bitmap, uint32_t nblocks, uint32_t max_chunks,
-                                             hipStream_t stream);
+                                             uint64_t* bitmap, uint32_t nblocks, hipStream_t stream);
 extern "C" hipError_t lz4mi_launch_ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                                uint32_t* out_len, int32_t* status, const uint32_t* chunk_base,

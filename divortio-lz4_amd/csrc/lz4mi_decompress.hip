@@ -1283,7 +1283,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 }
 
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block<false>(a); }
-__global__ __launch_bounds__(64, 4) void lz4mi_decompress_bm_kernel(DecArgs a) { decompress_block<true>(a); }
 
 }  // namespace lz4mi
 
@@ -1321,7 +1320,6 @@ extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t* in, const u
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, 0, 1, bitmap, chunk_base};
     if (nblocks == 0) return hipSuccess;
-    if (bitmap) hipLaunchKernelGGL(lz4mi::lz4mi_decompress_bm_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    else hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }

@@ -83,10 +83,12 @@ struct MapArgs {
     const uint32_t* in_len;
     const uint32_t* out_cap;
     uint32_t min_ratio;           // blocks compressed less than out_cap / in_len >= min_ratio are not mapped
-    const uint32_t* chunk_base;   // first chunk index of each block in `bitmap`
+    const uint32_t* chunk_base;   // first chunk index of each block in `bitmap` (kNoMap: block not mapped)
     uint64_t* bitmap;             // kWords words per chunk
     uint32_t nblocks;
 };
+
+constexpr uint32_t kNoMap = 0xFFFFFFFFu;   // chunk_base of a block the ring decoder does not take
 
 struct RingArgs {
     const uint8_t* in;
@@ -175,15 +177,56 @@ __device__ __forceinline__ int32_t next_token_at(const uint8_t* blk, int32_t p, 
     return q;
 }
 
+// Device-side plan of the two-pass decode (no host round trip): block b is taken by the
+// ring decoder when it is compressed at least min_ratio:1 and its chunks fit the bitmap
+// scratch (capacity chunks); chunk_base[b] = its first chunk (exclusive scan over the
+// taken blocks) or kNoMap. *needed = the chunks all eligible blocks would take, read back
+// lazily by the host to grow the scratch for later calls (host-mapped word).
+constexpr int kPlanThreads = 1024;
+__global__ __launch_bounds__(kPlanThreads) void lz4mi_ring_plan_kernel(const uint32_t* in_len, const uint32_t* out_cap,
+                                                                      uint32_t min_ratio, uint32_t nblocks,
+                                                                      uint64_t capacity, uint32_t* chunk_base,
+                                                                      uint32_t* needed) {
+    __shared__ uint64_t part[kPlanThreads / kWave];
+    __shared__ uint64_t carry_s;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    uint64_t carry = 0;
+    for (uint32_t t0 = 0; t0 < nblocks; t0 += kPlanThreads) {
+        const uint32_t b = t0 + tid;
+        uint64_t nch = 0;
+        bool elig = false;
+        if (b < nblocks) {
+            const uint64_t len = in_len[b];
+            elig = len * min_ratio <= (uint64_t)out_cap[b];
+            nch = elig ? (len + kC - 1) / kC : 0;
+        }
+        uint64_t x = nch;   // inclusive wave scan
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, kWave);
+            if (lane >= d) x += y;
+        }
+        if (lane == kWave - 1) part[wv] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (int w = 0; w < wv; ++w) before += part[w];
+        const uint64_t base = before + x - nch;
+        if (b < nblocks) chunk_base[b] = (elig && base + nch <= capacity) ? (uint32_t)base : kNoMap;
+        if (tid == kPlanThreads - 1) carry_s = before + x;
+        __syncthreads();
+        carry = carry_s;
+        __syncthreads();
+    }
+    if (tid == 0) *needed = carry > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)carry;
+}
+
+// One workgroup per block, one lane per 1 KiB chunk (looping over the block's chunks).
 __global__ __launch_bounds__(64) void lz4mi_token_map_kernel(MapArgs a) {
-    const uint32_t b = blockIdx.y;
-    if (b >= a.nblocks) return;
+    const uint32_t b = blockIdx.x;
+    if (b >= a.nblocks || a.chunk_base[b] == kNoMap) return;
     const int32_t len = (int32_t)a.in_len[b];
-    if ((uint64_t)len * a.min_ratio > (uint64_t)a.out_cap[b]) return;
-    const int32_t k = (int32_t)(blockIdx.x * 64 + threadIdx.x);
     const int32_t nch = (len + kC - 1) / kC;
-    if (k >= nch) return;
     const uint8_t* blk = a.in + a.in_off[b];
+    for (int32_t k = (int32_t)threadIdx.x; k < nch; k += 64) {
     uint64_t* bm = a.bitmap + ((uint64_t)a.chunk_base[b] + (uint64_t)k) * kWords;
     const int32_t base = k * kC;
     const int32_t end = base + kC < len ? base + kC : len;
@@ -205,6 +248,7 @@ __global__ __launch_bounds__(64) void lz4mi_token_map_kernel(MapArgs a) {
     while (wi < kWords) {
         bm[wi++] = word;
         word = 0;
+    }
     }
 }
 
@@ -763,7 +807,7 @@ __global__ __launch_bounds__(kThreads, 2) void lz4mi_ring_decode_kernel(RingArgs
     if (b >= a.nblocks) return;
     const uint8_t* blk = a.in + a.in_off[b];
     const int32_t len = (int32_t)a.in_len[b];
-    if ((uint64_t)len * a.min_ratio > (uint64_t)a.out_cap[b]) {   // single-pass kernel's block
+    if ((uint64_t)len * a.min_ratio > (uint64_t)a.out_cap[b] || a.chunk_base[b] == kNoMap) {   // single-pass kernel's block
         if (tid == 0) a.status[b] = kStatusRedo;
         return;
     }
@@ -1076,14 +1120,21 @@ extern "C" int lz4mi_debug_ring_prof(unsigned long long* out) {
 }
 #endif
 
+extern "C" hipError_t lz4mi_launch_ring_plan(const uint32_t* in_len, const uint32_t* out_cap, uint32_t min_ratio,
+                                             uint32_t nblocks, uint64_t capacity_chunks, uint32_t* chunk_base,
+                                             uint32_t* needed, hipStream_t stream) {
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4mi::ring::lz4mi_ring_plan_kernel, dim3(1), dim3(lz4mi::ring::kPlanThreads), 0, stream,
+                       in_len, out_cap, min_ratio, nblocks, capacity_chunks, chunk_base, needed);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t lz4mi_launch_token_map(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                              const uint32_t* out_cap, uint32_t min_ratio, const uint32_t* chunk_base,
-                                             uint64_t* bitmap, uint32_t nblocks, uint32_t max_chunks,
-                                             hipStream_t stream) {
-    if (nblocks == 0 || max_chunks == 0) return hipSuccess;
+                                             uint64_t* bitmap, uint32_t nblocks, hipStream_t stream) {
+    if (nblocks == 0) return hipSuccess;
     lz4mi::ring::MapArgs a{in, in_off, in_len, out_cap, min_ratio, chunk_base, bitmap, nblocks};
-    hipLaunchKernelGGL(lz4mi::ring::lz4mi_token_map_kernel, dim3((max_chunks + 63) / 64, nblocks), dim3(64), 0, stream,
-                       a);
+    hipLaunchKernelGGL(lz4mi::ring::lz4mi_token_map_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 

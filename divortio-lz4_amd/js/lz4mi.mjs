@@ -102,11 +102,42 @@ function prewarm(table, buf, dictLen) {
 }
 
 /**
+ * Streaming XXH32 — class XXHash32 (src/xxhash32/xxhash32Stateful.js:13-152) over the
+ * addon's host implementation (16-byte carry, `(totalLen + len) | 0` length). The state
+ * is a 56-byte Uint8Array owned by this object.
+ */
+export class XXHash32 {
+    constructor(seed = 0) {
+        this.seed = seed | 0;
+        this.state = native.xxh32Reset(this.seed >>> 0, 0);
+    }
+
+    update(input) {
+        native.xxh32Update(this.state, input);
+    }
+
+    digest() {
+        return native.xxh32Digest(this.state) >>> 0;
+    }
+}
+
+// Block checksums (FLG bit 0x10): XXH32 (spec convergence, seed 0) of each block's payload,
+// computed for all blocks of a frame in one batched GPU call over the frame bytes.
+function blockChecksums(buf, payOff, payLen) {
+    const n = payLen.length;
+    const hashes = new Uint32Array(n);
+    if (n > 0) native.xxh32Blocks(buf, payOff, payLen, 0, hashes, native.XXH_STANDARD);
+    return hashes;
+}
+
+/**
  * LZ4 frame compression: same signature, defaults and output bytes as the
  * reference's compressBuffer (src/buffer/bufferCompress.js:100-259).
+ * `blockChecksum` (an addition; the reference never writes them) sets FLG bit 0x10
+ * and follows every block with the XXH32 of its payload.
  */
 export function compress(input, dictionary = null, maxBlockSize = 4194304, blockIndependence = false,
-    contentChecksum = false, addContentSize = true, outputBuffer = null) {
+    contentChecksum = false, addContentSize = true, outputBuffer = null, blockChecksum = false) {
     const rawInput = ensureBuffer(input);
     let work = rawInput;
     let start = 0;
@@ -125,11 +156,13 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
     const len = rawInput.length | 0;
     const bd = blockId(maxBlockSize);
     const bsize = BLOCK_MAX_SIZES[bd] | 0;
-    const output = outputBuffer || new Uint8Array((19 + len + ((len / 255) | 0) + 64 + 8) | 0);
+    const output = outputBuffer || new Uint8Array((19 + len + ((len / 255) | 0) + 64 + 8 +
+        (blockChecksum ? 4 * (Math.ceil(len / bsize) + 1) : 0)) | 0);
     let op = 0;
     output[op++] = 0x04; output[op++] = 0x22; output[op++] = 0x4D; output[op++] = 0x18;
     let flg = 1 << 6;
     if (blockIndependence) flg |= 0x20;
+    if (blockChecksum) flg |= 0x10;
     if (contentChecksum) flg |= 0x04;
     if (dictId !== null) flg |= 0x01;
     if (addContentSize) flg |= 0x08;
@@ -148,16 +181,20 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
     if (dictLen > 0) prewarm(table, work, dictLen);
 
     const end = start + len;
+    const sums = [];    // [payload position, payload length] of every block (block checksums)
     const emit = (pos, n, compSize, bytes) => {
         if (compSize > 0 && compSize < n) {
             writeU32(output, compSize, op);
             output.set(bytes, op + 4);
+            if (blockChecksum) sums.push(op + 4, compSize);
             op += 4 + compSize;
         } else {
             writeU32(output, (n | 0x80000000) >>> 0, op);
             output.set(work.subarray(pos, pos + n), op + 4);
+            if (blockChecksum) sums.push(op + 4, n);
             op += 4 + n;
         }
+        if (blockChecksum) op += 4;
     };
     let pos = start;
     if (blockIndependence) {
@@ -197,6 +234,13 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
             pos += n;
         }
     }
+    if (blockChecksum && sums.length > 0) {
+        const nb = sums.length / 2;
+        const payOff = new Float64Array(nb), payLen = new Uint32Array(nb);
+        for (let b = 0; b < nb; b++) { payOff[b] = sums[2 * b]; payLen[b] = sums[2 * b + 1]; }
+        const h = blockChecksums(output, payOff, payLen);
+        for (let b = 0; b < nb; b++) writeU32(output, h[b], payOff[b] + payLen[b]);
+    }
     writeU32(output, 0, op); op += 4;
     if (contentChecksum) { writeU32(output, native.xxHash32(rawInput, 0), op); op += 4; }
     return output.subarray(0, op);
@@ -208,8 +252,11 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
  * reference's decompressBuffer (src/buffer/bufferDecompress.js:51-220).
  * Blocks of a known-size frame are decoded in one batched GPU call; a frame
  * whose blocks reference each other is decoded block by block.
+ * Block checksums (FLG 0x10) are skipped like the reference does (:191) unless
+ * `verifyBlockChecksum` (an addition) asks to check them: one batched GPU XXH32
+ * over all payloads; the first mismatching block throws "LZ4: Block Checksum Error".
  */
-export function decompress(input, dictionary = null, verifyChecksum = true) {
+export function decompress(input, dictionary = null, verifyChecksum = true, verifyBlockChecksum = false) {
     const data = ensureBuffer(input);
     const len = data.length | 0;
     let pos = 0;
@@ -241,6 +288,19 @@ export function decompress(input, dictionary = null, verifyChecksum = true) {
         blocks.push({ pos, raw: (bs & 0x80000000) !== 0, n: bs & 0x7FFFFFFF });
         pos += bs & 0x7FFFFFFF;
         if (hasBlockChecksum) pos += 4;
+    }
+    if (hasBlockChecksum && verifyBlockChecksum && blocks.length > 0) {
+        const nb = blocks.length;
+        const payOff = new Float64Array(nb), payLen = new Uint32Array(nb);
+        for (let b = 0; b < nb; b++) {
+            payOff[b] = blocks[b].pos;
+            payLen[b] = Math.max(0, Math.min(blocks[b].n, len - blocks[b].pos));
+        }
+        const h = blockChecksums(data, payOff, payLen);
+        for (let b = 0; b < nb; b++) {
+            const at = blocks[b].pos + blocks[b].n;
+            if (at + 4 > len || readU32(data, at) !== h[b]) throw new Error('LZ4: Block Checksum Error');
+        }
     }
 
     let result;
@@ -352,6 +412,381 @@ function batchDirect(data, blocks, result, dict, bmax) {
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Streaming encoder / decoder (src/shared/lz4Encode.js, src/shared/lz4Decode.js).
+
+// The reference's LZ4Encoder compresses a block into a Uint8Array(blockSize + 1028) at
+// offset 4 (lz4Encode.js:232-245); a literal run > 64 bytes that does not fit throws the
+// RangeError of output.set (blockCompress.js:100,198). A batch-compressed block is walked
+// to find that throw when its output overran the array (incompressible blocks > 261 KiB).
+function encoderOverflowThrows(comp, cap) {
+    let op = 4, ip = 0;
+    const n = comp.length;
+    while (ip < n) {
+        const tok = comp[ip++];
+        op++;
+        let lit = tok >>> 4;
+        if (lit === 15) {
+            let b;
+            do { b = comp[ip++]; lit += b; op++; } while (b === 255 && ip < n);
+        }
+        if (lit > 64 && op + lit > cap) return true;
+        op += lit;
+        ip += lit;
+        if (ip >= n) break;          // the final literals
+        ip += 2;
+        op += 2;
+        if ((tok & 15) === 15) {
+            let b;
+            do { b = comp[ip++]; op++; } while (b === 255 && ip < n);
+        }
+    }
+    return false;
+}
+
+function rangeError() { return new RangeError('Source is too large'); }
+
+function frameHeader(blockIndependence, contentChecksum, bdId, dictId) {   // lz4Encode.js:61-94
+    const h = new Uint8Array(15);
+    let p = 0;
+    writeU32(h, MAGIC, p); p += 4;
+    let flg = 1 << 6;
+    if (blockIndependence) flg |= 0x20;
+    if (contentChecksum) flg |= 0x04;
+    if (dictId) flg |= 0x01;
+    h[p++] = flg;
+    h[p++] = (bdId & 7) << 4;
+    if (dictId) { writeU32(h, dictId, p); p += 4; }
+    h[p] = (native.xxHash32(h.subarray(4, p), 0) >>> 8) & 0xFF;
+    p++;
+    return h.subarray(0, p);
+}
+
+/**
+ * Streaming frame encoder with the reference LZ4Encoder's API and output
+ * (src/shared/lz4Encode.js:96-340): add(chunk) returns the frame pieces ready so far
+ * (header, then one Uint8Array per block: size word + payload), finish() the rest
+ * (remaining blocks, EndMark, content checksum). Independent-block streams compress
+ * every block an add() completes in one batched GPU call; dependent streams carry the
+ * hash table and the 64 KiB window from block to block like the reference (one GPU call
+ * per block, the table rebased after each, :262-290).
+ */
+export class LZ4Encoder {
+    constructor(maxBlockSize = 4194304, blockIndependence = false, contentChecksum = false, dictionary = null) {
+        this.blockIndependence = blockIndependence;
+        this.contentChecksum = contentChecksum;
+        this.blockSize = BLOCK_MAX_SIZES[blockId(maxBlockSize)] || 4194304;
+        this.bdId = blockId(this.blockSize);
+        this.buffer = new Uint8Array(0);
+        this.hasWrittenHeader = false;
+        this.isClosed = false;
+        this.hashTable = new Int32Array(HASH_TABLE_SIZE);
+        this.dictSize = 0;
+        if (this.contentChecksum) this.hasher = new XXHash32(0);
+        this.dictId = null;
+        if (dictionary) {
+            // the reference chains digest() on update()'s undefined result (lz4Encode.js:130)
+            throw new TypeError("Cannot read property 'digest' of undefined");
+        }
+    }
+
+    add(chunk) {
+        if (this.isClosed) throw new Error('Stream is closed');
+        const data = ensureBuffer(chunk);
+        if (data.length === 0) return [];
+        if (this.contentChecksum) this.hasher.update(data);
+        const nb = new Uint8Array(this.buffer.length + data.length);
+        nb.set(this.buffer);
+        nb.set(data, this.buffer.length);
+        this.buffer = nb;
+        const results = [];
+        if (!this.hasWrittenHeader) {
+            results.push(frameHeader(this.blockIndependence, this.contentChecksum, this.bdId, this.dictId));
+            this.hasWrittenHeader = true;
+        }
+        if (this.blockIndependence) {
+            const n = Math.floor((this.buffer.length - this.dictSize) / this.blockSize);
+            if (n > 0) for (const b of this._flushIndependent(n, false)) results.push(b);
+        } else {
+            while (this.buffer.length >= this.dictSize + this.blockSize) results.push(this._flushDependent(false));
+        }
+        return results;
+    }
+
+    // n full blocks (or, final, everything left) of an independent stream in one batched call
+    _flushIndependent(n, final) {
+        const bs = this.blockSize;
+        const sizes = [];
+        let left = this.buffer.length - this.dictSize;
+        for (let b = 0; b < n || (final && left > 0); b++) {
+            const k = Math.min(bs, left);
+            sizes.push(k);
+            left -= k;
+        }
+        const nb = sizes.length;
+        const srcOff = new Float64Array(nb), srcLen = new Uint32Array(nb);
+        const outOff = new Float64Array(nb), outLen = new Uint32Array(nb);
+        let pos = this.dictSize, slot = 0;
+        for (let b = 0; b < nb; b++) {
+            srcOff[b] = pos; srcLen[b] = sizes[b]; outOff[b] = slot;
+            pos += sizes[b];
+            slot += sizes[b] + ((sizes[b] / 255) | 0) + 16;
+        }
+        const scratch = new Uint8Array(slot);
+        native.compressBlocks(this.buffer, srcOff, srcLen, scratch, outOff, outLen);
+        const out = [];
+        for (let b = 0; b < nb; b++) {
+            const k = sizes[b], c = outLen[b];
+            const comp = scratch.subarray(outOff[b], outOff[b] + c);
+            const cap = k + 1024 + 4;               // Uint8Array(maxOutputSize + 4), lz4Encode.js:232-233
+            if (c + 4 > cap && encoderOverflowThrows(comp, cap)) throw rangeError();
+            let rec;
+            if (c > 0 && c < k) {
+                rec = new Uint8Array(c + 4);
+                writeU32(rec, c, 0);
+                rec.set(comp, 4);
+            } else {
+                rec = new Uint8Array(k + 4);
+                writeU32(rec, (k | 0x80000000) >>> 0, 0);
+                rec.set(this.buffer.subarray(srcOff[b], srcOff[b] + k), 4);
+            }
+            out.push(rec);
+        }
+        this.buffer = this.buffer.subarray(pos);
+        this.dictSize = 0;
+        return out;
+    }
+
+    // lz4Encode.js:215-298 for a dependent stream: one block with the carried table
+    _flushDependent(final) {
+        const available = this.buffer.length - this.dictSize;
+        if (available === 0 && !final) return new Uint8Array(0);
+        let blockSize = this.blockSize;
+        if (available < blockSize) {
+            if (final) blockSize = available;
+            else return new Uint8Array(0);
+        }
+        const srcStart = this.dictSize;
+        const output = new Uint8Array(blockSize + 1024 + 4);
+        const compSize = native.compressBlock(this.buffer, output, srcStart, blockSize, this.hashTable, 4);
+        let rec;
+        if (compSize > 0 && compSize < blockSize) {
+            writeU32(output, compSize, 0);
+            rec = output.subarray(0, compSize + 4);
+        } else {
+            writeU32(output, (blockSize | 0x80000000) >>> 0, 0);
+            output.set(this.buffer.subarray(srcStart, srcStart + blockSize), 4);
+            rec = output.subarray(0, blockSize + 4);
+        }
+        const consumedEnd = srcStart + blockSize;
+        const preserveLen = Math.min(consumedEnd, WINDOW_SIZE);
+        const shift = consumedEnd - preserveLen;
+        this.buffer = this.buffer.subarray(shift);
+        this.dictSize = preserveLen;
+        const t = this.hashTable;
+        for (let i = 0; i < HASH_TABLE_SIZE; i++) t[i] = t[i] > shift ? t[i] - shift : 0;
+        return rec;
+    }
+
+    finish() {
+        if (this.isClosed) return [];
+        this.isClosed = true;
+        const frames = [];
+        if (!this.hasWrittenHeader)
+            frames.push(frameHeader(this.blockIndependence, this.contentChecksum, this.bdId, this.dictId));
+        if (this.blockIndependence) {
+            if (this.buffer.length - this.dictSize > 0) for (const b of this._flushIndependent(0, true)) frames.push(b);
+        } else {
+            while (this.buffer.length - this.dictSize > 0) frames.push(this._flushDependent(true));
+        }
+        const end = new Uint8Array(4);
+        frames.push(end);
+        if (this.contentChecksum && this.hasher) {
+            const b = new Uint8Array(4);
+            writeU32(b, this.hasher.digest(), 0);
+            frames.push(b);
+        }
+        return frames;
+    }
+}
+
+/**
+ * Streaming frame decoder with the reference LZ4Decoder's state machine and API
+ * (src/shared/lz4Decode.js:48-307): update(chunk) returns the decoded chunks of every
+ * block the input completes. The reference passes three arguments to decompressBlock
+ * (:232) and so throws on every compressed block (SURVEY F6); this decoder makes the
+ * six-argument call it evidently meant — decompressBlock(block, 0, n, workspace, 0,
+ * window) — so each chunk is what the reference's decompressBlock produces for it.
+ * The compressed blocks of an independent frame that one update() completes are
+ * decoded in one batched GPU call.
+ */
+export class LZ4Decoder {
+    constructor(dictionary = null, verifyChecksum = true) {
+        this.state = 0;
+        this.dictionary = dictionary ? ensureBuffer(dictionary) : null;
+        this.verifyChecksum = verifyChecksum;
+        this.blockIndependence = true;
+        this.hasBlockChecksum = false;
+        this.hasContentChecksum = false;
+        this.buffer = new Uint8Array(0);
+        this.hasher = null;
+        this.window = new Uint8Array(WINDOW_SIZE);
+        this.windowPos = 0;
+        if (this.dictionary) {
+            const size = Math.min(this.dictionary.length, WINDOW_SIZE);
+            this.window.set(this.dictionary.subarray(this.dictionary.length - size), 0);
+            this.windowPos = size;
+        }
+    }
+
+    update(chunk) {
+        if (this.buffer.length > 0) {
+            const nb = new Uint8Array(this.buffer.length + chunk.length);
+            nb.set(this.buffer);
+            nb.set(chunk, this.buffer.length);
+            this.buffer = nb;
+        } else {
+            this.buffer = chunk;
+        }
+        const output = [];
+        const pending = [];      // compressed blocks of an independent frame, decoded together
+        const flush = () => {
+            if (pending.length === 0) return;
+            const dec = this._decodeIndependent(pending);
+            for (let k = 0; k < pending.length; k++) {
+                if (pending[k].slot === null) continue;
+                output[pending[k].slot] = dec[k];
+                if (this.hasher) this.hasher.update(dec[k]);
+            }
+            pending.length = 0;
+        };
+        for (;;) {
+            if (this.state === 0) {                                   // magic
+                if (this.buffer.length < 4) break;
+                if (readU32(this.buffer, 0) !== MAGIC) { flush(); throw new Error('LZ4: Invalid Magic Number'); }
+                this.buffer = this.buffer.subarray(4);
+                this.state = 1;
+                this.hasher = this.verifyChecksum ? new XXHash32(0) : null;
+            }
+            if (this.state === 1) {                                   // header
+                if (this.buffer.length < 2) break;
+                const flg = this.buffer[0];
+                this.blockIndependence = (flg & 0x20) !== 0;
+                this.hasBlockChecksum = (flg & 0x10) !== 0;
+                const hasContentSize = (flg & 0x08) !== 0;
+                this.hasContentChecksum = (flg & 0x04) !== 0;
+                const hasDictId = (flg & 0x01) !== 0;
+                let need = 2 + (hasContentSize ? 8 : 0) + (hasDictId ? 4 : 0) + 1;
+                if (this.buffer.length < need) break;
+                if (hasDictId) {
+                    const expected = readU32(this.buffer, 2 + (hasContentSize ? 8 : 0));
+                    if (!this.dictionary) { flush(); throw new Error('LZ4: Archive requires a Dictionary, but none was provided.'); }
+                    const actual = native.xxHash32(this.dictionary, 0) >>> 0;
+                    if (actual !== expected) {
+                        flush();
+                        throw new Error(`LZ4: Dictionary ID Mismatch. Header: 0x${expected.toString(16)}, Provided: 0x${actual.toString(16)}`);
+                    }
+                }
+                this.buffer = this.buffer.subarray(need);
+                this.state = 2;
+            }
+            if (this.state === 2) {                                   // block size
+                if (this.buffer.length < 4) break;
+                const v = readU32(this.buffer, 0);
+                this.buffer = this.buffer.subarray(4);
+                if (v === 0) { this.state = 4; continue; }
+                this.isUncompressed = (v & 0x80000000) !== 0;
+                this.currentBlockSize = v & 0x7FFFFFFF;
+                this.state = 3;
+            }
+            if (this.state === 3) {                                   // block body
+                const need = this.currentBlockSize + (this.hasBlockChecksum ? 4 : 0);
+                if (this.buffer.length < need) break;
+                const blockData = this.buffer.subarray(0, this.currentBlockSize);
+                this.buffer = this.buffer.subarray(need);
+                if (this.blockIndependence && !this.isUncompressed) {
+                    pending.push({ data: blockData, slot: output.length });
+                    output.push(null);
+                } else {
+                    flush();
+                    let dec;
+                    if (this.isUncompressed) {
+                        dec = blockData.slice();
+                    } else {
+                        const dict = this.windowPos === WINDOW_SIZE ? this.window : this.window.subarray(0, this.windowPos);
+                        const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
+                        const w = native.decompressBlock(blockData, 0, blockData.length, ws, 0,
+                            this.blockIndependence ? null : dict, decodeFlags);
+                        dec = ws.slice(0, w);
+                    }
+                    output.push(dec);
+                    if (this.hasher) this.hasher.update(dec);
+                    if (!this.blockIndependence) this._updateWindow(dec);
+                }
+                this.state = 2;
+            }
+            if (this.state === 4) {                                   // content checksum
+                flush();
+                if (this.hasContentChecksum) {
+                    if (this.buffer.length < 4) break;
+                    if (this.verifyChecksum && this.hasher) {
+                        if (readU32(this.buffer, 0) !== this.hasher.digest()) throw new Error('LZ4: Content Checksum Error');
+                    }
+                    this.buffer = this.buffer.subarray(4);
+                }
+                this.state = 0;
+                this.hasher = null;
+                if (this.buffer.length === 0) break;
+            }
+        }
+        flush();
+        return output;
+    }
+
+    // independent compressed blocks, each as decompressBlock(block, 0, n, workspace, 0) decodes it
+    _decodeIndependent(blocks) {
+        const nb = blocks.length, cap = BLOCK_MAX_SIZES[7];
+        let total = 0;
+        for (const b of blocks) total += b.data.length;
+        const input = new Uint8Array(total);
+        const inOff = new Float64Array(nb), inLen = new Uint32Array(nb);
+        const outOff = new Float64Array(nb), outCap = new Uint32Array(nb);
+        const outLen = new Uint32Array(nb), status = new Int32Array(nb);
+        let p = 0;
+        for (let k = 0; k < nb; k++) {
+            input.set(blocks[k].data, p);
+            inOff[k] = p; inLen[k] = blocks[k].data.length;
+            outOff[k] = k * cap; outCap[k] = cap;
+            p += blocks[k].data.length;
+        }
+        const out = new Uint8Array(nb * cap);
+        native.decompressBlocks(input, inOff, inLen, out, outOff, outCap, outLen, status, null, decodeFlags);
+        const res = [];
+        for (let k = 0; k < nb; k++) {
+            if (status[k] === native.ERR_CROSS_BLOCK || status[k] !== 0) {
+                // a back-reference (or the F1 rewrite) before the block's start: decode it alone,
+                // into a fresh workspace, which also raises the reference's error if it has one
+                const ws = new Uint8Array(cap);
+                const w = native.decompressBlock(blocks[k].data, 0, blocks[k].data.length, ws, 0, null, decodeFlags);
+                res.push(ws.slice(0, w));
+            } else {
+                res.push(out.slice(outOff[k], outOff[k] + outLen[k]));
+            }
+        }
+        return res;
+    }
+
+    _updateWindow(chunk) {                                            // lz4Decode.js:279-306
+        const cl = chunk.length;
+        if (cl >= WINDOW_SIZE) { this.window.set(chunk.subarray(cl - WINDOW_SIZE), 0); this.windowPos = WINDOW_SIZE; return; }
+        if (this.windowPos + cl <= WINDOW_SIZE) { this.window.set(chunk, this.windowPos); this.windowPos += cl; return; }
+        const keep = WINDOW_SIZE - cl;
+        this.window.copyWithin(0, this.windowPos - keep, this.windowPos);
+        this.window.set(chunk, keep);
+        this.windowPos = WINDOW_SIZE;
+    }
+}
+
 export function xxHash32(input, seed = 0) {
     return native.xxHash32(ensureBuffer(input), seed);
 }
@@ -374,8 +809,12 @@ export const LZ4 = {
     compressBlocks,
     decompressBlocks,
     xxHash32,
+    XXHash32,
+    LZ4Encoder,
+    LZ4Decoder,
     setDecodeMode,
     version: native.version,
+    buildId: native.buildId,
 };
 
 export default LZ4;

@@ -20,12 +20,15 @@ LIB_PATH = os.path.join(PKG_DIR, "liblz4mi.so")
 OK = 0
 ERR_OUTPUT_TOO_SMALL, ERR_MALFORMED, ERR_OFFSET0, ERR_DICT_OOB = -1, -2, -3, -4
 ERR_MAGIC, ERR_VERSION, ERR_CHECKSUM, ERR_RANGE, ERR_CROSS_BLOCK = -5, -6, -7, -8, -9
+ERR_BLOCK_CHECKSUM = -10
 ERR_HIP, ERR_ARG, ERR_NO_DEVICE = -100, -101, -102
 
 DEVICE_PTRS = 0x1
 JS_COMPAT = 0x2
 JS_EXACT = 0x8
 XXH_STANDARD = 0x4
+XXH_LEN64 = 0x10
+BLOCK_CHECKSUM = 0x20
 
 GEN_RANDOM, GEN_REPETITIVE, GEN_TILES216 = 0, 1, 2
 GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GEN_TILES216}
@@ -33,7 +36,8 @@ GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GE
 # every symbol include/lz4mi.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_version",
            "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
-           "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks")
+           "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
+           "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest")
 
 
 class Lz4miError(RuntimeError):
@@ -62,6 +66,13 @@ def lib():
         L.lz4mi_status_message.restype = ctypes.c_char_p
         L.lz4mi_status_message.argtypes = [ctypes.c_int32]
         L.lz4mi_version.restype = ctypes.c_char_p
+        L.lz4mi_build_id.restype = ctypes.c_char_p
+        L.lz4mi_xxh32_reset.restype = None
+        L.lz4mi_xxh32_reset.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32]
+        L.lz4mi_xxh32_update.restype = None
+        L.lz4mi_xxh32_update.argtypes = [_vp, _vp, ctypes.c_size_t]
+        L.lz4mi_xxh32_digest.restype = ctypes.c_uint32
+        L.lz4mi_xxh32_digest.argtypes = [_vp]
         L.lz4mi_init.restype = ctypes.c_int32
         L.lz4mi_init.argtypes = [ctypes.c_int32]
         L.lz4mi_device_count.restype = ctypes.c_int32
@@ -103,6 +114,11 @@ def device_count():
     return lib().lz4mi_device_count()
 
 
+def build_id():
+    """Hash of the sources liblz4mi.so was compiled from (see Makefile SRC_HASH)."""
+    return lib().lz4mi_build_id().decode()
+
+
 def _p(a):
     return a.ctypes.data if a is not None and a.size else None
 
@@ -124,6 +140,25 @@ def xxh32(data, seed=0, standard=False):
     """xxHash32 (reference variant by default; host CPU, one serial chain)."""
     a = _u8(data)
     return lib().lz4mi_xxh32(_p(a), a.size, seed & 0xFFFFFFFF, XXH_STANDARD if standard else 0)
+
+
+class XXHash32:
+    """Streaming XXH32 (class XXHash32, src/xxhash32/xxhash32Stateful.js:13-152) over the
+    library's host implementation: update(chunk) any number of times, digest() any time.
+    len64=True keeps the 64-bit length (the reference wraps it at 2 GiB, :37)."""
+
+    def __init__(self, seed=0, standard=False, len64=False):
+        self._st = np.zeros(7, dtype=np.uint64)       # lz4mi_xxh32_state
+        lib().lz4mi_xxh32_reset(self._st.ctypes.data, seed & 0xFFFFFFFF,
+                                (XXH_STANDARD if standard else 0) | (XXH_LEN64 if len64 else 0))
+
+    def update(self, data):
+        a = _u8(data)
+        lib().lz4mi_xxh32_update(self._st.ctypes.data, _p(a), a.size)
+        return self
+
+    def digest(self):
+        return lib().lz4mi_xxh32_digest(self._st.ctypes.data)
 
 
 def compress_blocks(blocks):
@@ -157,10 +192,10 @@ def compress_raw(src, output, src_start, src_len, hash_table, output_offset):
     assert hash_table.dtype == np.int32 and hash_table.size == 16384 and hash_table.flags.c_contiguous
     assert output.dtype == np.uint8 and output.flags.c_contiguous
     r = lib().lz4mi_compress_block_table(_p(s), s.size, src_start, src_len, hash_table.ctypes.data,
-                                         _p(output), output.size, output_offset, 0, None)
+                                         _p(output), output.size, output_offset or 0, 0, None)
     if r < 0:
         raise Lz4miError(int(r))
-    return int(r)
+    return 0 if output_offset is None else int(r)   # (dIndex - undefined) | 0 (blockCompress.js:232)
 
 
 def _dec_flags(js_compat, js_exact):
@@ -256,7 +291,9 @@ def generate_blocks_dev(out_ptr, kind, seed0, block_size, nblocks, stream=0):
 
 
 def frame_pack_dev(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr, rec_off_ptr,
-                   nblocks, stream=0):
-    """Device-side frame block records (size word + compressed or stored payload) at rec_off."""
+                   nblocks, stream=0, block_checksum=False):
+    """Device-side frame block records (size word + compressed or stored payload [+ XXH32 of
+    the payload with block_checksum]) at rec_off."""
     _check(lib().lz4mi_frame_pack(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr,
-                                  rec_off_ptr, nblocks, DEVICE_PTRS, stream or None))
+                                  rec_off_ptr, nblocks, DEVICE_PTRS | (BLOCK_CHECKSUM if block_checksum else 0),
+                                  stream or None))

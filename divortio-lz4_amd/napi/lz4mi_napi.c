@@ -17,9 +17,13 @@
  *   decompressBlocks(input, inOff: Float64Array, inLen: Uint32Array, output, outOff: Float64Array,
  *                    outCap: Uint32Array, outLen: Uint32Array, status: Int32Array, dictionary?, flags?)
  *       the block loop of decompressBuffer (src/buffer/bufferDecompress.js:133-192), batched
- *   xxHash32(input, seed) -> uint32       src/xxhash32/xxhash32.js:21
- *   statusMessage(code) -> string; init(device) -> status; version() -> string
- *   constants: JS_COMPAT, JS_EXACT, XXH_STANDARD
+ *   xxHash32(input, seed, flags?) -> uint32       src/xxhash32/xxhash32.js:21
+ *   xxh32Reset(seed, flags?) -> Uint8Array state; xxh32Update(state, input); xxh32Digest(state) -> uint32
+ *       class XXHash32 src/xxhash32/xxhash32Stateful.js:13-152 (state in a caller-owned Uint8Array)
+ *   xxh32Blocks(input, off: Float64Array, len: Uint32Array, seed, hashes: Uint32Array, flags?)
+ *       batched XXH32 of independent buffers on the GPU (frame block checksums, FLG 0x10)
+ *   statusMessage(code) -> string; init(device) -> status; version() -> string; buildId() -> string
+ *   constants: JS_COMPAT, JS_EXACT, XXH_STANDARD, XXH_LEN64, ERR_CROSS_BLOCK
  *
  * Offsets are passed as Float64Array (exact up to 2^53) so one call can span
  * buffers larger than 4 GiB.
@@ -98,8 +102,18 @@ static napi_value make_i64(napi_env env, int64_t v) {
 }
 
 static napi_value throw_status(napi_env env, int64_t st) {
-    napi_throw_error(env, NULL, lz4mi_status_message((int32_t)st));
+    if (st == LZ4MI_ERR_RANGE)   /* the reference's TypedArray.set RangeError */
+        napi_throw_range_error(env, NULL, lz4mi_status_message((int32_t)st));
+    else
+        napi_throw_error(env, NULL, lz4mi_status_message((int32_t)st));
     return NULL;
+}
+
+static int is_undefined(napi_env env, size_t argc, napi_value* argv, size_t i) {
+    napi_valuetype t;
+    if (argc <= i) return 1;
+    if (napi_typeof(env, argv[i], &t) != napi_ok) return 0;
+    return t == napi_undefined;
 }
 
 /* compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset) */
@@ -128,6 +142,8 @@ static napi_value n_compress_block(napi_env env, napi_callback_info info) {
                                            (uint8_t*)out.data, out.length, to_i32(ooff), 0, NULL);
     if (!tab.data) free(table);
     if (r < 0) return throw_status(env, r);
+    /* without outputOffset the reference returns (dIndex - undefined) | 0 == 0 (blockCompress.js:37,232) */
+    if (is_undefined(env, argc, argv, 5)) return make_i64(env, 0);
     return make_i64(env, r);
 }
 
@@ -159,17 +175,30 @@ static napi_value n_decompress_block(napi_env env, napi_callback_info info) {
     return make_i64(env, out_len);
 }
 
+/* Block offsets: a Float64Array whose entries are integers in [0, 2^53) (anything else
+ * would be undefined behaviour to convert and could wrap the bounds checks below). */
 static int f64_offsets(napi_env env, const view_t* v, uint32_t n, uint64_t* dst, const char* what) {
+    char msg[128];
     if (v->type != napi_float64_array || v->length < n) {
-        char msg[128];
         snprintf(msg, sizeof msg, "lz4mi: %s must be a Float64Array of block offsets", what);
         napi_throw_type_error(env, NULL, msg);
         return 0;
     }
     const double* d = (const double*)v->data;
-    for (uint32_t b = 0; b < n; ++b) dst[b] = (uint64_t)d[b];
+    for (uint32_t b = 0; b < n; ++b) {
+        const double x = d[b];
+        if (!(x >= 0.0 && x < 9007199254740992.0) || x != (double)(uint64_t)x) {
+            snprintf(msg, sizeof msg, "lz4mi: %s[%u] is not an integer offset in [0, 2^53)", what, b);
+            napi_throw_range_error(env, NULL, msg);
+            return 0;
+        }
+        dst[b] = (uint64_t)x;
+    }
     return 1;
 }
+
+/* off + len <= total, without overflow */
+static int in_bounds(uint64_t off, uint64_t len, uint64_t total) { return off <= total && len <= total - off; }
 
 static int u32_array(napi_env env, const view_t* v, uint32_t n, int want_int32, const char* what) {
     napi_typedarray_type t = want_int32 ? napi_int32_array : napi_uint32_array;
@@ -203,7 +232,8 @@ static napi_value n_compress_blocks(napi_env env, napi_callback_info info) {
     }
     const uint32_t* lens = (const uint32_t*)slen.data;
     for (uint32_t b = 0; b < n; ++b) {
-        if (offs[b] + lens[b] > src.length || offs[n + b] + lz4mi_compress_bound(lens[b]) > out.length) {
+        if (!in_bounds(offs[b], lens[b], src.length) ||
+            !in_bounds(offs[n + b], lz4mi_compress_bound(lens[b]), out.length)) {
             free(offs);
             return throw_status(env, LZ4MI_ERR_ARG);
         }
@@ -242,7 +272,7 @@ static napi_value n_decompress_blocks(napi_env env, napi_callback_info info) {
     const uint32_t* il = (const uint32_t*)ilen.data;
     const uint32_t* oc = (const uint32_t*)ocap.data;
     for (uint32_t b = 0; b < n; ++b) {
-        if (offs[b] + il[b] > in.length || offs[n + b] + oc[b] > out.length) {
+        if (!in_bounds(offs[b], il[b], in.length) || !in_bounds(offs[n + b], oc[b], out.length)) {
             free(offs);
             return throw_status(env, LZ4MI_ERR_ARG);
         }
@@ -276,6 +306,95 @@ static napi_value n_xxh32(napi_env env, napi_callback_info info) {
     return r;
 }
 
+/* xxh32Reset(seed, flags?) -> Uint8Array holding an lz4mi_xxh32_state */
+static napi_value n_xxh32_reset(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    int64_t seed = 0, flags = 0;
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc > 0 && !get_i64(env, argv[0], &seed)) return NULL;
+    if (argc > 1 && !get_i64(env, argv[1], &flags)) return NULL;
+    napi_value ab, ta;
+    void* data = NULL;
+    CHECK(napi_create_arraybuffer(env, sizeof(lz4mi_xxh32_state), &data, &ab));
+    lz4mi_xxh32_reset((lz4mi_xxh32_state*)data, (uint32_t)seed, (uint32_t)flags);
+    CHECK(napi_create_typedarray(env, napi_uint8_array, sizeof(lz4mi_xxh32_state), ab, 0, &ta));
+    return ta;
+}
+
+static lz4mi_xxh32_state* get_state(napi_env env, napi_value v) {
+    view_t st;
+    if (!get_view(env, v, &st, 1, "state")) return NULL;
+    if (st.type != napi_uint8_array || st.length != sizeof(lz4mi_xxh32_state) || ((uintptr_t)st.data & 7)) {
+        napi_throw_type_error(env, NULL, "lz4mi: state must come from xxh32Reset");
+        return NULL;
+    }
+    return (lz4mi_xxh32_state*)st.data;
+}
+
+/* xxh32Update(state, input) */
+static napi_value n_xxh32_update(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    lz4mi_xxh32_state* st = get_state(env, argv[0]);
+    if (!st) return NULL;
+    view_t in;
+    if (!get_view(env, argv[1], &in, 1, "input")) return NULL;
+    if (in.type != napi_uint8_array && in.type != napi_uint8_clamped_array && in.type != napi_int8_array) {
+        napi_throw_type_error(env, NULL, "lz4mi: input must be a Uint8Array");
+        return NULL;
+    }
+    lz4mi_xxh32_update(st, (const uint8_t*)in.data, in.length);
+    return NULL;
+}
+
+/* xxh32Digest(state) -> uint32 */
+static napi_value n_xxh32_digest(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    lz4mi_xxh32_state* st = get_state(env, argv[0]);
+    if (!st) return NULL;
+    napi_value r;
+    CHECK(napi_create_uint32(env, lz4mi_xxh32_digest(st), &r));
+    return r;
+}
+
+/* xxh32Blocks(input, off: Float64Array, len: Uint32Array, seed, hashes: Uint32Array, flags?) -> 0 */
+static napi_value n_xxh32_blocks(napi_env env, napi_callback_info info) {
+    size_t argc = 6;
+    napi_value argv[6];
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    view_t in, off, len, hs;
+    int64_t seed = 0, flags = 0;
+    if (!get_view(env, argv[0], &in, 1, "input") || !get_view(env, argv[1], &off, 1, "off") ||
+        !get_view(env, argv[2], &len, 1, "len") || !get_view(env, argv[4], &hs, 1, "hashes"))
+        return NULL;
+    if (!get_i64(env, argv[3], &seed)) return NULL;
+    if (argc > 5 && !get_i64(env, argv[5], &flags)) return NULL;
+    uint32_t n = (uint32_t)len.length;
+    if (!u32_array(env, &len, n, 0, "len") || !u32_array(env, &hs, n, 0, "hashes")) return NULL;
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+    if (!offs) return throw_status(env, LZ4MI_ERR_ARG);
+    if (!f64_offsets(env, &off, n, offs, "off")) {
+        free(offs);
+        return NULL;
+    }
+    const uint32_t* l = (const uint32_t*)len.data;
+    for (uint32_t b = 0; b < n; ++b) {
+        if (!in_bounds(offs[b], l[b], in.length)) {
+            free(offs);
+            return throw_status(env, LZ4MI_ERR_ARG);
+        }
+    }
+    int32_t st = lz4mi_xxh32_blocks((const uint8_t*)in.data, offs, l, (uint32_t)seed, (uint32_t*)hs.data, n,
+                                    (uint32_t)flags & LZ4MI_XXH_STANDARD, NULL);
+    free(offs);
+    if (st) return throw_status(env, st);
+    return make_i64(env, 0);
+}
+
 static napi_value n_status_message(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -303,6 +422,13 @@ static napi_value n_version(napi_env env, napi_callback_info info) {
     return r;
 }
 
+static napi_value n_build_id(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value r;
+    CHECK(napi_create_string_utf8(env, lz4mi_build_id(), NAPI_AUTO_LENGTH, &r));
+    return r;
+}
+
 static napi_value n_device_count(napi_env env, napi_callback_info info) {
     (void)info;
     return make_i64(env, lz4mi_device_count());
@@ -315,6 +441,11 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"compressBlocks", NULL, n_compress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"decompressBlocks", NULL, n_decompress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"xxHash32", NULL, n_xxh32, NULL, NULL, NULL, napi_default, NULL},
+        {"xxh32Reset", NULL, n_xxh32_reset, NULL, NULL, NULL, napi_default, NULL},
+        {"xxh32Update", NULL, n_xxh32_update, NULL, NULL, NULL, napi_default, NULL},
+        {"xxh32Digest", NULL, n_xxh32_digest, NULL, NULL, NULL, napi_default, NULL},
+        {"xxh32Blocks", NULL, n_xxh32_blocks, NULL, NULL, NULL, napi_default, NULL},
+        {"buildId", NULL, n_build_id, NULL, NULL, NULL, napi_default, NULL},
         {"statusMessage", NULL, n_status_message, NULL, NULL, NULL, napi_default, NULL},
         {"init", NULL, n_init, NULL, NULL, NULL, napi_default, NULL},
         {"version", NULL, n_version, NULL, NULL, NULL, napi_default, NULL},
@@ -323,7 +454,7 @@ static napi_value Init(napi_env env, napi_value exports) {
     if (napi_define_properties(env, exports, sizeof fns / sizeof fns[0], fns) != napi_ok) return NULL;
     const struct { const char* name; int64_t v; } consts[] = {
         {"JS_COMPAT", LZ4MI_JS_COMPAT}, {"JS_EXACT", LZ4MI_JS_EXACT}, {"XXH_STANDARD", LZ4MI_XXH_STANDARD},
-        {"ERR_CROSS_BLOCK", LZ4MI_ERR_CROSS_BLOCK},
+        {"XXH_LEN64", LZ4MI_XXH_LEN64}, {"ERR_CROSS_BLOCK", LZ4MI_ERR_CROSS_BLOCK},
     };
     for (size_t i = 0; i < sizeof consts / sizeof consts[0]; ++i) {
         napi_value v;

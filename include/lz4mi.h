@@ -37,10 +37,15 @@ extern "C" {
 #define LZ4MI_ERR_MAGIC (-5)            /* "LZ4: Invalid Magic Number"     src/buffer/bufferDecompress.js:60 */
 #define LZ4MI_ERR_VERSION (-6)          /* "LZ4: Unsupported Version v"    src/buffer/bufferDecompress.js:67 */
 #define LZ4MI_ERR_CHECKSUM (-7)         /* "LZ4: Content Checksum Error"   src/buffer/bufferDecompress.js:216 */
-#define LZ4MI_ERR_RANGE (-8)            /* RangeError of TypedArray.set (stored block overflow) */
+#define LZ4MI_ERR_RANGE (-8)            /* RangeError "Source is too large" of TypedArray.set: a literal run
+                                           > 64 bytes that does not fit `output` (blockCompress.js:100,198),
+                                           a stored block past the result (bufferDecompress.js) */
 #define LZ4MI_ERR_CROSS_BLOCK (-9)      /* batched decode only: a back-reference reaches before the block's
                                            own output (not an independent block); the frame layer then
                                            decodes the frame's blocks in order, one call per block */
+#define LZ4MI_ERR_BLOCK_CHECKSUM (-10)  /* a frame block's checksum (FLG bit 0x10) does not match its payload;
+                                           reported only when block-checksum verification is asked for (the
+                                           reference skips them: src/buffer/bufferDecompress.js:191) */
 #define LZ4MI_ERR_HIP (-100)            /* a HIP runtime call failed */
 #define LZ4MI_ERR_ARG (-101)            /* invalid argument (size limits, NULL pointers) */
 #define LZ4MI_ERR_NO_DEVICE (-102)      /* no usable gfx950 device */
@@ -55,6 +60,10 @@ extern "C" {
                                     double-copy-tail rewrite (F1) would change a byte; only those blocks are
                                     decoded again by the serial reference-exact kernel. */
 
+#define LZ4MI_XXH_LEN64 0x10u    /* streaming XXH32: keep the 64-bit total length (streams over 2 GiB);
+                                    default: the reference class's `(totalLen + len) | 0` */
+#define LZ4MI_BLOCK_CHECKSUM 0x20u /* lz4mi_frame_pack: records carry XXH32 (spec) of their payload (FLG 0x10) */
+
 /* Largest block the kernels accept (the reference's largest block size is 4 MiB;
  * raw calls may pass more, up to 2^31-1 like the reference's `|0` arithmetic). */
 #define LZ4MI_MAX_BLOCK 0x7FFFFFFFu
@@ -65,10 +74,14 @@ static inline uint64_t lz4mi_compress_bound(uint64_t n) { return n + n / 255u + 
 /* Human-readable message of a status (the reference's exact error string). */
 const char* lz4mi_status_message(int32_t status);
 
-/* Device selection / info. Returns LZ4MI_OK or LZ4MI_ERR_*. */
+/* Device selection / info. Returns LZ4MI_OK or LZ4MI_ERR_*. lz4mi_init(-1) keeps the
+ * current device (or HIP's current one); another device releases every buffer of the old one. */
 int32_t lz4mi_init(int32_t device);
 int32_t lz4mi_device_count(void);
 const char* lz4mi_version(void);
+/* Hash of the sources the library was compiled from (Makefile SRC_HASH): lets a test
+ * prove the loaded binary was built from the tree beside it. */
+const char* lz4mi_build_id(void);
 
 /*
  * Batched raw-block DECOMPRESS.
@@ -130,6 +143,21 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
 uint32_t lz4mi_xxh32(const uint8_t* data, size_t len, uint32_t seed, uint32_t flags);
 
 /*
+ * Streaming XXH32, on the host CPU.
+ * Replaces: class XXHash32 src/xxhash32/xxhash32Stateful.js:13-152 — update() carries up to
+ * 15 bytes between calls (:34-68); digest() (:110-152) does not change the state. The
+ * length is kept as the class keeps it, `(totalLen + len) | 0` tested signed (:37, :113),
+ * unless flags has LZ4MI_XXH_LEN64; LZ4MI_XXH_STANDARD selects the spec convergence.
+ * The state is a plain 56-byte struct owned by the caller (no allocation).
+ */
+typedef struct lz4mi_xxh32_state {
+    uint64_t opaque[7];
+} lz4mi_xxh32_state;
+void lz4mi_xxh32_reset(lz4mi_xxh32_state* state, uint32_t seed, uint32_t flags);
+void lz4mi_xxh32_update(lz4mi_xxh32_state* state, const uint8_t* data, size_t len);
+uint32_t lz4mi_xxh32_digest(const lz4mi_xxh32_state* state);
+
+/*
  * Batched XXH32 of independent buffers on the GPU (per-block checksums,
  * dictionary ids, parity digests). hashes[b] = xxHash32(in[off[b] .. +len[b]), seed).
  */
@@ -142,6 +170,9 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
  * block b's record goes to frame[rec_off[b] ..): LE32 comp_len[b] and the compressed bytes
  * comp[comp_off[b] ..) when 0 < comp_len[b] < raw_len[b], else LE32 (raw_len[b] | 0x80000000) and the
  * raw bytes raw[raw_off[b] ..). rec_off is the exclusive prefix sum of the record sizes (4 + payload).
+ * flags & LZ4MI_BLOCK_CHECKSUM: each record ends with LE32 XXH32 (spec, seed 0) of its payload,
+ * the block checksum of the LZ4 frame format (FLG bit 0x10; record size 8 + payload), which the
+ * reference's reader skips (src/buffer/bufferDecompress.js:191) and its writer never emits.
  * Device pointers only (flags must include LZ4MI_DEVICE_PTRS); async on `stream`.
  */
 int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len, const uint8_t* comp,

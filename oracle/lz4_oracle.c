@@ -284,10 +284,13 @@ static inline void wr32(sink_t* s, uint32_t v) { put(s, v & 255); put(s, (v >> 8
 int64_t orc_frame_bound(int64_t len) { return 19 + len + len / 255 + 64 + 8; }
 
 /* bufferCompress.js:100-259: LZ4 frame writer. Dictionary prewarm uses the
- * reference's Jenkins-style hash (:191-203), not the block hash. */
-int64_t orc_compress_frame(const uint8_t* in, int64_t len, const uint8_t* dict, int64_t dict_len,
-                           int64_t max_block, int32_t indep, int32_t checksum, int32_t add_size,
-                           uint8_t* out, int64_t out_cap) {
+ * reference's Jenkins-style hash (:191-203), not the block hash.
+ * block_checksum (not in the reference, whose reader skips them, bufferDecompress.js:191):
+ * FLG bit 0x10 and, after each block's payload, LE32 XXH32 (spec) of the payload — the
+ * LZ4 frame format's block checksum. */
+int64_t orc_compress_frame_ex(const uint8_t* in, int64_t len, const uint8_t* dict, int64_t dict_len,
+                              int64_t max_block, int32_t indep, int32_t checksum, int32_t add_size,
+                              int32_t block_checksum, uint8_t* out, int64_t out_cap) {
     sink_t s = { out, out_cap, 0 };
     int64_t win = 0;
     uint8_t* work = (uint8_t*)in;
@@ -304,7 +307,8 @@ int64_t orc_compress_frame(const uint8_t* in, int64_t len, const uint8_t* dict, 
     int bd = block_id(max_block);
     int32_t bsize = kBlockMax[bd];
     put(&s, 0x04); put(&s, 0x22); put(&s, 0x4D); put(&s, 0x18);
-    uint8_t flg = 0x40 | (indep ? 0x20 : 0) | (checksum ? 0x04 : 0) | (has_dict ? 0x01 : 0) | (add_size ? 0x08 : 0);
+    uint8_t flg = 0x40 | (indep ? 0x20 : 0) | (checksum ? 0x04 : 0) | (has_dict ? 0x01 : 0) | (add_size ? 0x08 : 0) |
+                  (block_checksum ? 0x10 : 0);
     put(&s, flg);
     put(&s, (uint8_t)((bd & 7) << 4));
     if (add_size) { wr32(&s, (uint32_t)len); wr32(&s, (uint32_t)((uint64_t)len >> 32)); }
@@ -340,6 +344,10 @@ int64_t orc_compress_frame(const uint8_t* in, int64_t len, const uint8_t* dict, 
             s.pos = size_pos; wr32(&s, (uint32_t)n | 0x80000000u);
             for (int32_t k = 0; k < n; ++k) put(&s, work[pos + k]);
         }
+        if (block_checksum) {
+            const int64_t pay = size_pos + 4, plen = s.pos - pay;
+            wr32(&s, (pay + plen <= out_cap) ? orc_xxh32_std(out + pay, (uint64_t)plen, 0) : 0);
+        }
         if (indep) memset(table, 0, 16384 * sizeof(int32_t));
         pos = e;
     }
@@ -348,6 +356,12 @@ int64_t orc_compress_frame(const uint8_t* in, int64_t len, const uint8_t* dict, 
     free(table);
     if (has_dict) free(work);
     return s.pos;
+}
+
+int64_t orc_compress_frame(const uint8_t* in, int64_t len, const uint8_t* dict, int64_t dict_len,
+                           int64_t max_block, int32_t indep, int32_t checksum, int32_t add_size,
+                           uint8_t* out, int64_t out_cap) {
+    return orc_compress_frame_ex(in, len, dict, dict_len, max_block, indep, checksum, add_size, 0, out, out_cap);
 }
 
 /* bufferDecompress.js:51-220. Writes into `out` (capacity out_cap) and

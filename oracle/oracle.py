@@ -55,6 +55,10 @@ def lib():
                                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, _i64p]
         L.orc_frame_bound.restype = ctypes.c_int64
         L.orc_frame_bound.argtypes = [ctypes.c_int64]
+        L.orc_compress_frame_ex.restype = ctypes.c_int64
+        L.orc_compress_frame_ex.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
         L.orc_compress_frame.restype = ctypes.c_int64
         L.orc_compress_frame.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -166,14 +170,14 @@ def decompress_block(comp, out_size, in_off=0, in_size=None, out=None, out_off=0
 
 
 def compress_frame(data, dictionary=None, max_block_size=4194304, block_independence=False,
-                   content_checksum=False, add_content_size=True):
+                   content_checksum=False, add_content_size=True, block_checksum=False):
     a = _u8(data)
     d = _u8(dictionary)
-    cap = lib().orc_frame_bound(a.size) + 64
+    cap = lib().orc_frame_bound(a.size) + 64 + (4 * (a.size // 65536 + 2) if block_checksum else 0)
     out = np.zeros(cap, dtype=np.uint8)
-    n = lib().orc_compress_frame(_ptr(a), a.size, _ptr(d), 0 if d is None else d.size, max_block_size,
-                                 int(bool(block_independence)), int(bool(content_checksum)),
-                                 int(bool(add_content_size)), _ptr(out), cap)
+    n = lib().orc_compress_frame_ex(_ptr(a), a.size, _ptr(d), 0 if d is None else d.size, max_block_size,
+                                    int(bool(block_independence)), int(bool(content_checksum)),
+                                    int(bool(add_content_size)), int(bool(block_checksum)), _ptr(out), cap)
     return out[:n].copy()
 
 

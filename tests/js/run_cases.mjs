@@ -107,4 +107,107 @@ for (const c of job.cases) {
         });
     }
 }
+
+function concat(parts) {
+    const total = parts.reduce((a, b) => a + b.length, 0);
+    const all = new Uint8Array(total);
+    let o = 0;
+    for (const x of parts) { all.set(x, o); o += x.length; }
+    return all;
+}
+
+for (const c of job.cases) {
+    if (c.op === 'raw_edge') {
+        // F7 (five arguments -> 0) and the RangeError of output.set (blockCompress.js:37,100,198,232)
+        check(c.id, () => {
+            const src = read(c.src);
+            const out = new Uint8Array(c.out_len);
+            const table = new Int32Array(16384);
+            let r, err = null;
+            try {
+                r = c.five_args ? LZ4.compressRaw(src, out, c.start, c.len, table)
+                    : LZ4.compressRaw(src, out, c.start, c.len, table, c.out_off);
+            } catch (e) { err = e; }
+            if (c.ok) {
+                if (err) return 'threw ' + err.message;
+                if (r !== c.value) return `returned ${r}, expected ${c.value}`;
+            } else {
+                if (!err) return 'did not throw';
+                if (err.name !== c.error_name || err.message !== c.error) return `threw ${err.name}: ${err.message}`;
+            }
+            if (!Buffer.from(out).equals(Buffer.from(read(c.out_ref)))) return 'output bytes differ';
+            if (!Buffer.from(table.buffer).equals(Buffer.from(read(c.table_ref)))) return 'table differs';
+            return true;
+        });
+    } else if (c.op === 'xxh32_stateful') {
+        check(c.id, () => {
+            const base = read(c.src);
+            for (const [n, chunk, seed, h] of c.rows) {
+                const st = new LZ4.XXHash32(seed);
+                for (let p = 0; p < n; p += chunk) st.update(base.subarray(p, Math.min(n, p + chunk)));
+                if (hex(st.digest()) !== h) return `n=${n} chunk=${chunk}: ${hex(st.digest())} != ${h}`;
+            }
+            return true;
+        });
+    } else if (c.op === 'stream') {
+        // LZ4Encoder (lz4Encode.js) fed the same chunks: the same pieces, bytes and errors
+        check(c.id, () => {
+            const input = read(c.src);
+            const enc = new LZ4.LZ4Encoder(c.block, c.indep, c.checksum);
+            const parts = [];
+            let err = null;
+            try {
+                for (let p = 0; p < input.length; p += c.chunk)
+                    for (const x of enc.add(input.subarray(p, Math.min(input.length, p + c.chunk)))) parts.push(x.slice());
+                for (const x of enc.finish()) parts.push(x.slice());
+            } catch (e) { err = e.name + ': ' + e.message; }
+            if (err !== c.error) return `error ${err} != ${c.error}`;
+            const lens = parts.map((x) => x.length);
+            if (JSON.stringify(lens) !== JSON.stringify(c.part_lens)) return `pieces ${lens} != ${c.part_lens}`;
+            if (err) return true;
+            const all = concat(parts);
+            if (hex(LZ4.xxHash32(all, 0)) !== c.stream_xxh) return 'stream bytes differ';
+            // LZ4Decoder (the call lz4Decode.js:232 meant) in 50 KB pieces; spec mode round-trips
+            for (const mode of ['reference', 'spec']) {
+                LZ4.setDecodeMode(mode);
+                try {
+                    const d = new LZ4.LZ4Decoder(null, mode === 'spec' || c.roundtrip_equals_input);
+                    const outs = [];
+                    for (let p = 0; p < all.length; p += 50000)
+                        for (const x of d.update(all.subarray(p, Math.min(all.length, p + 50000)))) outs.push(x);
+                    const back = concat(outs);
+                    if ((mode === 'spec' || c.roundtrip_equals_input) && !Buffer.from(back).equals(Buffer.from(input)))
+                        return `LZ4Decoder (${mode}) output differs from the input`;
+                    const f = LZ4.decompress(all, null, mode === 'spec' || c.roundtrip_equals_input);
+                    if (!Buffer.from(f).equals(Buffer.from(back))) return `LZ4Decoder (${mode}) != decompress`;
+                } finally {
+                    LZ4.setDecodeMode('reference');
+                }
+            }
+            return true;
+        });
+    } else if (c.op === 'bcs') {
+        // block checksums: skipped by default like the reference; written and verified on request
+        check(c.id, () => {
+            const g = read(c.frame);
+            const back = LZ4.decompress(g);
+            if (hex(LZ4.xxHash32(back, 0)) !== c.dec_xxh) return 'skip decode differs from the reference';
+            const bad = expectThrow(() => LZ4.decompress(g, null, true, true), 'LZ4: Block Checksum Error');
+            if (bad !== true) return 'golden frame (marker checksums): ' + bad;
+            const data = read(c.src);
+            const f = LZ4.compress(data, null, c.block, true, false, true, null, true);
+            if (f.length !== c.ours_len || hex(LZ4.xxHash32(f, 0)) !== c.ours_xxh) return 'frame with block checksums != oracle';
+            LZ4.setDecodeMode('spec');
+            try {
+                const rt = LZ4.decompress(f, null, true, true);
+                if (!Buffer.from(rt).equals(Buffer.from(data))) return 'verified round trip differs';
+            } finally {
+                LZ4.setDecodeMode('reference');
+            }
+            const f2 = f.slice();
+            f2[f2.length - 5] ^= 0x40;      // last block's checksum
+            return expectThrow(() => LZ4.decompress(f2, null, true, true), 'LZ4: Block Checksum Error');
+        });
+    }
+}
 process.stdout.write(JSON.stringify(results) + '\n');

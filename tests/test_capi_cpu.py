@@ -67,3 +67,63 @@ def test_gpu_entry_points_fail_loudly_without_device():
     assert ei.value.status == lz4mi.ERR_NO_DEVICE
     with pytest.raises(lz4mi.Lz4miError):
         lz4mi.decompress_blocks([np.array([0x10, 1], dtype=np.uint8)], [1])
+
+
+def source_hash():
+    """The Makefile's SRC_HASH: sha256 of SRC then HDR, in Makefile order, first 16 hex digits."""
+    import hashlib
+    pkg = os.path.join(ROOT, "divortio-lz4_amd")
+    with open(os.path.join(pkg, "Makefile")) as f:
+        mk = f.read()
+    files = []
+    for var in ("SRC", "HDR"):
+        files += re.search(r"^%s := (.*)$" % var, mk, flags=re.M).group(1).split()
+    h = hashlib.sha256()
+    for name in files:
+        with open(os.path.join(pkg, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def test_loaded_library_was_built_from_this_tree():
+    """Build provenance: the library's compiled-in source hash equals the hash of the
+    sources beside it (a stale liblz4mi.so fails here, on CPU and on the GPU box)."""
+    assert lz4mi.build_id() == source_hash()
+    assert lz4mi.build_id() in lz4mi.lib().lz4mi_version().decode()
+
+
+def test_streaming_xxh32_matches_reference_class(manifest):
+    """lz4mi_xxh32_reset/update/digest vs class XXHash32 (xxhash32Stateful.js) on the golden chunkings."""
+    (g,) = cases_of(manifest, "xxh32_stateful")
+    base = O.generate(g["input"]["gen"], g["input"]["seed"], g["input"]["n"])
+    for n, chunk, seed, h in g["rows"]:
+        st = lz4mi.XXHash32(seed)
+        for p in range(0, n, chunk):
+            st.update(base[p:min(n, p + chunk)])
+        assert "%08x" % st.digest() == h, (n, chunk)
+        assert st.digest() == lz4mi.xxh32(base[:n], seed)          # digest() leaves the state unchanged
+    seed, n, h = g["empty_updates"]
+    st = lz4mi.XXHash32(seed)
+    for part in (base[:0], base[:5], base[:0], base[5:n]):
+        st.update(part)
+    assert "%08x" % st.digest() == h
+    (c,) = cases_of(manifest, "xxh32")
+    st = lz4mi.XXHash32(0)
+    for p in range(0, 1000, 37):
+        st.update(base[:0])
+    gen = O.generate(c["input"]["gen"], c["input"]["seed"], 1000)
+    st = lz4mi.XXHash32(0)
+    for p in range(0, 1000, 37):
+        st.update(gen[p:p + 37])
+    assert "%08x" % st.digest() == c["stateful_1000"]
+
+
+def test_streaming_xxh32_length_modes():
+    """The class wraps totalLen at 2^32 and tests it signed (:37,:113); LEN64 keeps the full
+    length. Both agree below 2 GiB, and with the spec convergence flag match the spec digest."""
+    data = O.generate("random", 5, 5000)
+    for std in (False, True):
+        a = lz4mi.XXHash32(3, standard=std).update(data).digest()
+        b = lz4mi.XXHash32(3, standard=std, len64=True).update(data).digest()
+        assert a == b == lz4mi.xxh32(data, 3, standard=std)
+    assert lz4mi.XXHash32(0, standard=True).update(data).digest() == O.xxh32_std(data)

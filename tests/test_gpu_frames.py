@@ -1,0 +1,232 @@
+"""GPU parity for the BASELINE configs beyond the single-GPU block batch, and the
+C-ABI behaviours added in round 2. Everything runs through liblz4mi.so and is
+checked against the pinned oracle (bit-exact).
+
+  config 4  a complete independent frame (header, device records, EndMark,
+            content xxh32) built by lz4mi.frame from device-compressed blocks
+  config 5  the 50/50 random/tiles216 mix, shuffled and clustered, compressed and
+            decoded on the GPU, per-block digests against the oracle
+  plus      compressRaw's RangeError/F7 semantics, block checksums, unaligned
+            device xxh32, two concurrent streams, the ring decoder's bitmap overflow
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import cases_of, golden_bytes
+
+lz4mi = pytest.importorskip("lz4mi")
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+BLOCK = 4 << 20
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    lz4mi.init(0)
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def test_library_is_built_from_this_tree():
+    from test_capi_cpu import source_hash
+    assert lz4mi.build_id() == source_hash()
+
+
+def test_config4_complete_frame_64mib():
+    """64 MiB of tiles216 (16 x 4 MiB blocks): lz4mi.frame.compress_frame_sharded (batch
+    encoder + lz4mi_frame_pack + header/EndMark/streamed content xxh32) == the oracle's
+    LZ4.compress(x, null, 4 MiB, true, true) byte for byte; the sharded decode returns x."""
+    from lz4mi import frame as F
+    n = 16
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    lz4mi.generate_blocks_dev(raw.data_ptr(), "tiles216", 1, BLOCK, n, _stream())
+    torch.cuda.synchronize()
+    host = raw.cpu().numpy()
+    ref = O.compress_frame(host, None, BLOCK, True, True, True)
+    got = F.compress_frame_sharded(raw, BLOCK, content_checksum=True)
+    torch.cuda.synchronize()
+    assert got.numel() == ref.size
+    assert np.array_equal(got.cpu().numpy(), ref)
+    back = F.decompress_frame_sharded(ref, verify_checksum=True)
+    assert np.array_equal(back.numpy(), host)
+
+
+def test_frame_with_block_checksums_matches_oracle():
+    """Device records with FLG 0x10 block checksums (lz4mi_frame_pack + in-place XXH32) ==
+    the oracle's frame; a ragged last block and a stored (random) block included."""
+    from lz4mi import frame as F
+    data = np.concatenate([O.generate("tiles216", 21, 700000), O.generate("random", 22, 300000),
+                           O.generate("repetitive", 23, 90001)])
+    raw = torch.from_numpy(data.copy()).cuda()
+    for bs, cs in ((65536, False), (262144, True)):
+        ref = O.compress_frame(data, None, bs, True, cs, True, block_checksum=True)
+        got = F.compress_frame_sharded(raw, bs, content_checksum=cs, block_checksum=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), ref), bs
+
+
+def _mix_kinds(n, clustered):
+    if clustered:
+        from lz4mi import shard
+        return shard.clustered_mix_kinds(n)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench.mix_order(n)
+
+
+@pytest.mark.parametrize("clustered", [False, True])
+def test_config5_mix_encode_decode_vs_oracle(clustered):
+    """Config 5's 50/50 random/tiles216 mix (Fisher-Yates by xorshift32(0x5EED), or the
+    first half random): GPU compressed bytes == the oracle's for every block, GPU decode
+    == the input, in one batch each."""
+    n = 32
+    kinds = _mix_kinds(n, clustered)
+    assert kinds.count("random") == n // 2
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+    for b, k in enumerate(kinds):
+        lz4mi.generate_blocks_dev(tmp.data_ptr(), k, 1 + b, BLOCK, 1, _stream())
+        raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+    torch.cuda.synchronize()
+    host = raw.cpu().numpy()
+    # oracle: all blocks on host threads
+    in_off = np.arange(n, dtype=np.uint64) * np.uint64(BLOCK)
+    in_len = np.full(n, BLOCK, dtype=np.uint32)
+    slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
+    oc = np.zeros(n * slot, dtype=np.uint8)
+    o_off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    o_cap = np.full(n, slot, dtype=np.uint32)
+    o_len, st = O.blocks_mt(1, host, in_off, in_len, oc, o_off, o_cap, 8)
+    assert (st == 0).all()
+    # GPU
+    dev = "cuda"
+    r_off = torch.arange(n, dtype=torch.int64, device=dev) * BLOCK
+    r_len = torch.full((n,), BLOCK, dtype=torch.int32, device=dev)
+    comp = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    c_off = torch.arange(n, dtype=torch.int64, device=dev) * slot
+    c_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.compress_blocks_dev(raw.data_ptr(), r_off.data_ptr(), r_len.data_ptr(), comp.data_ptr(), c_off.data_ptr(),
+                              c_len.data_ptr(), n, _stream())
+    dec = torch.zeros(n * BLOCK, dtype=torch.uint8, device=dev)
+    d_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.decompress_blocks_dev(comp.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), dec.data_ptr(), r_off.data_ptr(),
+                                r_len.data_ptr(), d_len.data_ptr(), d_st.data_ptr(), n, _stream())
+    torch.cuda.synchronize()
+    cl = c_len.cpu().numpy()
+    ch = comp.cpu().numpy()
+    for b in range(n):
+        assert cl[b] == o_len[b], (b, kinds[b])
+        s = int(o_off[b])
+        assert np.array_equal(ch[b * slot:b * slot + cl[b]], oc[s:s + o_len[b]]), (b, kinds[b])
+    assert (d_st == 0).all() and (d_len == BLOCK).all()
+    assert torch.equal(dec, raw)
+
+
+def test_compress_raw_rangeerror_and_five_args(manifest):
+    """compressBlock's throw (RangeError of output.set on a literal run > 64 that does not
+    fit, blockCompress.js:100,198) and F7 (no outputOffset -> returns 0): the GPU table
+    kernel leaves the same output bytes and table as the reference."""
+    (g,) = cases_of(manifest, "compress_raw_edges")
+    for c in g["cases"]:
+        src = golden_bytes(c["src_file"]).copy()
+        out = np.zeros(c["out_len"], dtype=np.uint8)
+        table = np.zeros(16384, dtype=np.int32)
+        if c["ok"]:
+            r = lz4mi.compress_raw(src, out, c["start"], c["len"], table, None if c["five_args"] else c["out_off"])
+            assert r == c["value"], c["name"]
+        else:
+            with pytest.raises(lz4mi.Lz4miError) as ei:
+                lz4mi.compress_raw(src, out, c["start"], c["len"], table, c["out_off"])
+            assert ei.value.status == lz4mi.ERR_RANGE and str(ei.value) == c["error"], c["name"]
+        assert np.array_equal(out, golden_bytes(c["out_file"])), c["name"]
+        assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_file"])), c["name"]
+
+
+def test_xxh32_device_unaligned_buffers():
+    """lz4mi_xxh32_blocks on device pointers at odd offsets (the kernel's byte-load path)."""
+    src = O.generate("random", 12, 70000)
+    lens = [4095, 4096, 4111, 4112, 8191, 8192, 8193, 12345, 0, 1, 15, 16, 17]
+    stride = 9000
+    buf = np.zeros(stride * len(lens) + 64, dtype=np.uint8)
+    offs = []
+    for b, n in enumerate(lens):
+        o = b * stride + (b % 4) + (1 if b % 3 == 0 else 0)
+        buf[o:o + n] = src[b * 100:b * 100 + n]
+        offs.append(o)
+    d = torch.from_numpy(buf).cuda()
+    off = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    ln = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    for std in (False, True):
+        h = torch.zeros(len(lens), dtype=torch.int32, device="cuda")
+        lz4mi.xxh32_blocks_dev(d.data_ptr(), off.data_ptr(), ln.data_ptr(), h.data_ptr(), len(lens), 7, _stream(),
+                               standard=std)
+        torch.cuda.synchronize()
+        for b, n in enumerate(lens):
+            want = (O.xxh32_std if std else O.xxh32)(buf[offs[b]:offs[b] + n], 7)
+            assert (int(h[b]) & 0xFFFFFFFF) == want, (b, n, std)
+
+
+def test_two_streams_concurrently_bit_exact():
+    """Device-pointer calls on two streams at once: per-stream scratch (hash tables, ring
+    bitmaps) keeps both exact; no call blocks the host (the include/lz4mi.h contract)."""
+    n = 24
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    jobs = []
+    for k, (s, kind) in enumerate(((s1, "tiles216"), (s2, "repetitive"))):
+        raw = torch.empty(n * (1 << 20), dtype=torch.uint8, device="cuda")
+        lz4mi.generate_blocks_dev(raw.data_ptr(), kind, 40 + k, 1 << 20, n, s.cuda_stream)
+        jobs.append((s, kind, raw))
+    torch.cuda.synchronize()
+    outs = []
+    for s, kind, raw in jobs:
+        bs = 1 << 20
+        slot = (lz4mi.compress_bound(bs) + 255) & ~255
+        with torch.cuda.stream(s):
+            r_off = torch.arange(n, dtype=torch.int64, device="cuda") * bs
+            r_len = torch.full((n,), bs, dtype=torch.int32, device="cuda")
+            comp = torch.zeros(n * slot, dtype=torch.uint8, device="cuda")
+            c_off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+            c_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+            dec = torch.zeros(n * bs, dtype=torch.uint8, device="cuda")
+            d_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+            d_st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        outs.append((s, raw, r_off, r_len, comp, c_off, c_len, dec, d_len, d_st))
+    torch.cuda.synchronize()
+    for _ in range(3):      # interleave the two streams' enqueues
+        for s, raw, r_off, r_len, comp, c_off, c_len, dec, d_len, d_st in outs:
+            lz4mi.compress_blocks_dev(raw.data_ptr(), r_off.data_ptr(), r_len.data_ptr(), comp.data_ptr(),
+                                      c_off.data_ptr(), c_len.data_ptr(), n, s.cuda_stream)
+        for s, raw, r_off, r_len, comp, c_off, c_len, dec, d_len, d_st in outs:
+            lz4mi.decompress_blocks_dev(comp.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), dec.data_ptr(),
+                                        r_off.data_ptr(), r_len.data_ptr(), d_len.data_ptr(), d_st.data_ptr(), n,
+                                        s.cuda_stream)
+    torch.cuda.synchronize()
+    for (s, kind, _), (_, raw, r_off, r_len, comp, c_off, c_len, dec, d_len, d_st) in zip(jobs, outs):
+        assert (d_st == 0).all() and torch.equal(dec, raw), kind
+        host = raw[: 1 << 20].cpu().numpy()
+        assert np.array_equal(comp[:int(c_len[0])].cpu().numpy(), O.compress_block_bytes(host)), kind
+
+
+def test_ring_decoder_bitmap_overflow_falls_back_exactly(monkeypatch):
+    """When the device plan cannot fit every ring-eligible block in the bitmap scratch, the
+    blocks past it go to the single-pass kernel: same bytes, no host round trip."""
+    monkeypatch.setenv("LZ4MI_RING_MAX_CHUNKS", "12")
+    n, bs = 8, 1 << 20                 # repetitive 1 MiB blocks: ~5 chunks each (4 KiB compressed)
+    raw = torch.empty(n * bs, dtype=torch.uint8, device="cuda")
+    lz4mi.generate_blocks_dev(raw.data_ptr(), "repetitive", 3, bs, n, _stream())
+    srcs = [raw[b * bs:(b + 1) * bs].cpu().numpy() for b in range(n)]
+    comps = [O.compress_block_bytes(x) for x in srcs]
+    st, outs, _ = lz4mi.decompress_blocks(comps, [bs] * n)
+    assert (st == 0).all()
+    for s, o in zip(srcs, outs):
+        assert np.array_equal(s, o)

@@ -70,6 +70,112 @@ def _worker(rank, world, port, q):
         q.put((rank, False, False, repr(e)))
 
 
+class _OracleCodec:
+    """Each rank's block codec stand-in on CPU (the GPU path is lz4mi.frame.DeviceCodec):
+    the oracle compresses the blocks; lz4mi.shard lays out the records."""
+
+    def records(self, raw, block_size, block_checksum):
+        import torch
+        import oracle as O
+        from lz4mi import shard
+        a = raw.numpy()
+        parts = []
+        for p in range(0, a.size, block_size):
+            blk = a[p:p + block_size]
+            rec = shard.block_records([blk], [O.compress_block_bytes(blk)])
+            parts.append(rec)
+            if block_checksum:
+                parts.append(np.array([O.xxh32_std(rec[4:])], dtype="<u4").view(np.uint8))
+        return torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8))
+
+
+def _oracle_decode(comp, block_max):
+    import oracle as O
+    outs = []
+    for c, stored in comp:
+        if stored:
+            outs.append(np.asarray(c))
+        else:
+            st, w, out = O.decompress_block(c, block_max)
+            assert st == 0
+            outs.append(out[:w])
+    return outs
+
+
+def _frame_worker(rank, world, port, q):
+    """lz4mi.frame (the product's sharded frame path) under gloo: records gathered to the
+    root, header, EndMark and the streamed content checksum must give the reference frame."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "oracle"), os.path.join(root, "divortio-lz4_amd")]
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from lz4mi import frame as F, shard
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        F.CHECKSUM_PIECE = 100003                      # several pieces per shard, odd size
+        data = np.concatenate([O.generate("tiles216", 18, 700000), O.generate("random", 19, 300000),
+                               O.generate("repetitive", 20, 90000)])
+        res = []
+        for bsize, bcs in ((65536, False), (262144, True)):
+            nb = -(-data.size // bsize)
+            lo, hi = shard.shard_range(nb, rank, world)
+            mine = torch.from_numpy(data[lo * bsize:min(data.size, hi * bsize)].copy())
+            got = F.compress_frame_sharded(mine, bsize, True, True, bcs, codec=_OracleCodec())
+            ref = O.compress_frame(data, None, bsize, True, True, True, block_checksum=bcs)
+            ok = True
+            if rank == 0:
+                ok = got is not None and np.array_equal(got.numpy(), ref)
+            else:
+                ok = got is None
+            back = F.decompress_frame_sharded(ref, True, decode=_oracle_decode)
+            ok_back = (back is not None and np.array_equal(back.numpy(), data)) if rank == 0 else back is None
+            res.append((ok, ok_back))
+        q.put((rank, res))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_sharded_frame_with_content_checksum_world2():
+    """BASELINE config 4's exchange on CPU: a whole independent frame (header + every
+    rank's records + EndMark + content xxh32, with and without block checksums) built
+    by lz4mi.frame across 2 ranks equals the oracle's frame byte for byte, and the
+    sharded decode of it gives the input back on the root."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_frame_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert isinstance(r[1], list), r
+        assert all(a and b for a, b in r[1]), r
+
+
+def test_frame_header_matches_reference_bytes(manifest):
+    """lz4mi.frame.header == the header of the reference's frames (bufferCompress.js:147-178)."""
+    from lz4mi import frame as F
+    from conftest import golden_bytes
+    (g,) = [c for c in manifest["cases"] if c["kind"] == "frames"]
+    seen = 0
+    for f in g["frames"]:
+        if not f.get("frame_file") or "dict" in f or "dict_text" in f:
+            continue
+        fr = golden_bytes(f["frame_file"])
+        size = f["n"] if f.get("add_size", True) else None
+        h = F.header(f["block"], f["indep"], f["checksum"], size)
+        assert bytes(fr[:len(h)]) == h, f
+        seen += 1
+    assert seen > 20
+
+
 def test_shard_range_covers_blocks():
     from lz4mi import shard
     for n in (0, 1, 7, 16, 4096):

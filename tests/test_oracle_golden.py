@@ -198,3 +198,58 @@ def test_xxh32_stateful_chunkings(manifest):
         assert "%08x" % O.xxh32_stateful(chunks, seed) == h, (n, chunk)
     seed, n, h = g["empty_updates"]
     assert "%08x" % O.xxh32_stateful([base[:0], base[:5], base[:0], base[5:n]], seed) == h
+
+
+def test_block_checksum_frames_are_skipped_like_the_reference(manifest):
+    """Frames with FLG bit 0x10 decode exactly as the reference decodes them (it skips the
+    checksums, bufferDecompress.js:191)."""
+    (g,) = cases_of(manifest, "block_checksum_skip")
+    for c in g["cases"]:
+        frame = golden_bytes(c["frame_file"])
+        st, out = O.decompress_frame(frame, js_compat=True)
+        assert st == 0 and c["dec_ok"], c["input"]
+        assert "%08x" % O.xxh32(out) == c["dec_xxh"], c["input"]
+
+
+def _liblz4_decode_frame(frame, cap):
+    """Decode an LZ4 frame with the system liblz4 (LZ4F API, verifies block checksums)."""
+    import ctypes
+    L = ctypes.CDLL("liblz4.so.1")
+    ctx = ctypes.c_void_p()
+    assert L.LZ4F_createDecompressionContext(ctypes.byref(ctx), 100) == 0
+    out = np.zeros(cap, dtype=np.uint8)
+    src = np.ascontiguousarray(frame)
+    dst_size = ctypes.c_size_t(cap)
+    src_size = ctypes.c_size_t(src.size)
+    L.LZ4F_decompress.restype = ctypes.c_size_t
+    r = L.LZ4F_decompress(ctx, out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(dst_size),
+                          src.ctypes.data_as(ctypes.c_void_p), ctypes.byref(src_size), None)
+    L.LZ4F_isError.restype = ctypes.c_uint
+    err = L.LZ4F_isError(ctypes.c_size_t(r))
+    L.LZ4F_freeDecompressionContext(ctx)
+    return err, out[:dst_size.value]
+
+
+def test_block_checksum_frames_interoperate_with_liblz4():
+    """Block checksums are the LZ4 frame format's (spec XXH32 of the payload): liblz4 1.9.3
+    verifies them. A corrupted checksum must be rejected by it."""
+    pytest.importorskip("ctypes")
+    try:
+        import ctypes
+        ctypes.CDLL("liblz4.so.1")
+    except OSError:
+        pytest.skip("liblz4 not installed")
+    data = np.concatenate([O.generate("tiles216", 3, 200000), O.generate("random", 4, 70000),
+                           O.generate("repetitive", 5, 90000)])
+    for bs in (65536, 262144):
+        f = O.compress_frame(data, None, bs, True, False, True, block_checksum=True)
+        assert f[4] & 0x10
+        err, out = _liblz4_decode_frame(f, data.size + 1024)
+        assert err == 0 and np.array_equal(out, data), bs
+        bad = f.copy()
+        bad[-8] ^= 1                      # last block's checksum (before the EndMark)
+        err, _ = _liblz4_decode_frame(bad, data.size + 1024)
+        assert err != 0, bs
+        # the reference-style reader skips them and decodes the same bytes
+        st, back = O.decompress_frame(f)
+        assert st == 0 and np.array_equal(back, data)

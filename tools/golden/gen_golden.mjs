@@ -303,6 +303,43 @@ for (const [name, src, genSpec] of blockInputs) {
     manifest.cases.push({ kind: 'streams', streams });
 }
 
+// ---- 10. block checksums: the reference reader skips them (bufferDecompress.js:191) ----
+{
+    // A reference frame re-laid with FLG bit 0x10 and a 4-byte slot after every block
+    // payload (filled with a marker: the reference never reads it), header checksum
+    // recomputed with the reference's xxHash32. Our reader must skip them the same way.
+    const cases = [];
+    for (const [iname, input, bsz] of [['tiles216', gen('tiles216', 61, 300000), 65536], ['text', gen('text', 62, 200000), 65536],
+        ['random', gen('random', 63, 100000), 65536]]) {
+        const f = compressBuffer(input, null, bsz, true, false);
+        const parts = [];
+        let pos = 6 + 8;                       // magic, FLG, BD, content size: HC at 14
+        const hdr = Uint8Array.from(f.subarray(0, pos + 1));
+        hdr[4] |= 0x10;
+        hdr[pos] = (xxHash32(hdr.subarray(4, pos), 0) >>> 8) & 0xFF;
+        parts.push(hdr);
+        pos += 1;
+        let k = 0;
+        for (;;) {
+            const v = (f[pos] | (f[pos + 1] << 8) | (f[pos + 2] << 16) | (f[pos + 3] << 24)) >>> 0;
+            if (v === 0) { parts.push(f.subarray(pos, pos + 4)); break; }
+            const n = v & 0x7FFFFFFF;
+            parts.push(f.subarray(pos, pos + 4 + n));
+            parts.push(Uint8Array.from([0xA5, k & 255, 0x5A, 0xC3]));
+            pos += 4 + n;
+            k++;
+        }
+        const total = parts.reduce((a, b) => a + b.length, 0);
+        const g = new Uint8Array(total);
+        let o = 0; for (const x of parts) { g.set(x, o); o += x.length; }
+        const back = tryCall(() => decompressBuffer(g));
+        cases.push({ input: iname, n: input.length, block: bsz, frame_file: save(g, `bcs_frame_${iname}`), blocks: k,
+            dec_ok: back.ok, dec_equals_input: back.ok && back.value.length === input.length && back.value.every((v, i) => v === input[i]),
+            dec_xxh: back.ok ? hex(xxHash32(back.value)) : null, gen: { gen: iname, seed: iname === 'tiles216' ? 61 : iname === 'text' ? 62 : 63, n: input.length } });
+    }
+    manifest.cases.push({ kind: 'block_checksum_skip', cases });
+}
+
 fs.writeFileSync(path.join(OUT, 'manifest.json'), JSON.stringify(manifest, null, 1));
 console.log('wrote', manifest.cases.length, 'case groups to', OUT);
 }

@@ -1,0 +1,35 @@
+// End-to-end rates of the drop-in JS layer (host buffers through N-API: H2D +
+// kernels + D2H + JS frame assembly), as a caller of the reference's API sees them.
+//   node tools/napi_e2e.mjs <input file> [reps] [dependent-mode bytes]
+// Prints one JSON line: LZ4.compress with independent blocks (batched), LZ4.compress
+// with the reference's default dependent blocks (one GPU call per block, the table
+// carried), LZ4.decompress in 'spec' and 'reference' (default) modes.
+import fs from 'fs';
+import { LZ4 } from '../divortio-lz4_amd/js/lz4mi.mjs';
+
+const input = new Uint8Array(fs.readFileSync(process.argv[2]));
+const reps = Number(process.argv[3] || 3);
+const depBytes = Math.min(input.length, Number(process.argv[4] || (16 << 20)));
+const now = () => Number(process.hrtime.bigint()) / 1e9;
+const rate = (bytes, fn, n) => {
+    fn();                                 // warm-up
+    const t0 = now();
+    for (let r = 0; r < n; r++) fn();
+    return +(bytes * n / (now() - t0) / 1e9).toFixed(3);
+};
+const out = { bytes: input.length };
+let frame = LZ4.compress(input, null, 4194304, true, false);
+out.ratio = +(input.length / frame.length).toFixed(3);
+out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, 4194304, true, false); }, reps);
+const dep = input.subarray(0, depBytes);
+out.compress_dependent_default_GBps = rate(dep.length, () => LZ4.compress(dep), 1);
+out.dependent_bytes = dep.length;
+for (const mode of ['spec', 'reference']) {
+    LZ4.setDecodeMode(mode);
+    const back = LZ4.decompress(frame);
+    if (Buffer.compare(Buffer.from(back), Buffer.from(input)) !== 0) throw new Error(`${mode} round trip mismatch`);
+    out[`decompress_${mode}_GBps`] = rate(input.length, () => LZ4.decompress(frame), reps);
+}
+LZ4.setDecodeMode('reference');
+out.note = 'host buffers through N-API (PCIe-inclusive): not the device-resident bench value';
+console.log(JSON.stringify(out));
