@@ -112,7 +112,9 @@ int32_t ensure_init() {
     return lz4mi_init(-1);
 }
 
-hipStream_t pick_stream(void* s) { return s ? static_cast<hipStream_t>(s) : g_ctx.stream; }
+// Device-pointer calls run on the caller's stream; NULL is HIP's default stream (what
+// torch reports for its default stream), so work is ordered with the caller's kernels.
+hipStream_t pick_stream(void* s) { return static_cast<hipStream_t>(s); }
 
 StreamCtx* stream_ctx(hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_ctx.streams_mu);

@@ -119,6 +119,7 @@ __device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int6
 __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t anchor, int64_t lit,
                                  uint32_t mnib, bool& range) {
     uint32_t tok = (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib;
+    const int64_t tok_pos = op;
     if (lane == 0) put_byte(j, op, tok);
     ++op;
     if (lit >= 15) {
@@ -129,6 +130,8 @@ __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t
         op += nff + 1;
     }
     if (lit > 64 && (uint64_t)(op + lit) > j.dst_total) {
+        // the reference ORs the match-length nibble into the token after the literal copy
+        if (lane == 0) put_byte(j, tok_pos, 0xF0u);
         range = true;
         return op;
     }

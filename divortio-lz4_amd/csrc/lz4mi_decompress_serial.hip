@@ -11,7 +11,12 @@
 
 namespace lz4mi {
 
-__device__ void decode_block_jscompat(const DecArgs& a, uint32_t b) {
+// isolated: the block is one of a batch decoded in parallel (the F1 redo of LZ4MI_JS_EXACT):
+// bytes before its own output may still be in flight, so a read or rewrite there is
+// reported (LZ4MI_ERR_CROSS_BLOCK) and the caller decodes the block alone, in order.
+constexpr int32_t kCrossBlock = -9;   // LZ4MI_ERR_CROSS_BLOCK
+
+__device__ void decode_block_jscompat(const DecArgs& a, uint32_t b, bool isolated) {
     const uint8_t* in = a.in + a.in_off[b];
     const int64_t iend = a.in_len[b];
     uint8_t* out = a.out;                       // absolute positions
@@ -51,6 +56,10 @@ __device__ void decode_block_jscompat(const DecArgs& a, uint32_t b) {
             continue;
         }
         int64_t start = op;
+        if (isolated && (from < oo || (off >= 8 && ml < 8 && start + ml - 8 - (int64_t)off < oo))) {
+            st = kCrossBlock;
+            break;
+        }
         for (int64_t k = 0; k < ml; ++k) {
             int64_t r = op - off;
             uint8_t v = r < olen ? out[r] : 0;
@@ -71,13 +80,13 @@ __device__ void decode_block_jscompat(const DecArgs& a, uint32_t b) {
 
 __global__ __launch_bounds__(64) void lz4mi_decompress_jscompat_kernel(DecArgs a) {
     if (threadIdx.x != 0) return;
-    for (uint32_t b = 0; b < a.nblocks; ++b) decode_block_jscompat(a, b);
+    for (uint32_t b = 0; b < a.nblocks; ++b) decode_block_jscompat(a, b, false);
 }
 
 __global__ __launch_bounds__(64) void lz4mi_decompress_redo_kernel(DecArgs a) {
     const uint32_t b = blockIdx.x;
     if (threadIdx.x != 0 || b >= a.nblocks || a.status[b] != kStatusF1) return;
-    decode_block_jscompat(a, b);
+    decode_block_jscompat(a, b, a.isolate != 0);
 }
 
 }  // namespace lz4mi

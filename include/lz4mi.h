@@ -13,8 +13,10 @@
  *    like the reference's functions).
  *  - With LZ4MI_DEVICE_PTRS every pointer (data AND the per-block descriptor
  *    arrays) is DEVICE memory, the call only enqueues work on `stream`
- *    (a hipStream_t; NULL = the library's per-device stream) and returns;
- *    status/out_len are valid once the stream has been synchronised.
+ *    (a hipStream_t; NULL = HIP's default stream) and returns without waiting
+ *    for the device or reading anything back; status/out_len are valid once the
+ *    stream has been synchronised. Scratch memory is per stream, so calls on
+ *    different streams may run concurrently.
  *  - Status codes: 0 = OK, negative = the reference's error (one per message,
  *    see lz4mi_status_message), <= -100 = infrastructure failure.
  */
