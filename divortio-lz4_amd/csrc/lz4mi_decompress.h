@@ -18,20 +18,17 @@ struct DecArgs {
     int32_t* status;
     uint32_t nblocks;
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
-    int f1check;   // flag blocks the reference's F1 rewrite would change (status kStatusF1)
+    int f1check;   // reference-exact (LZ4MI_JS_EXACT): fix up every chunk the reference's F1 rewrite changes
     int redo_only; // decode only the blocks whose status is kStatusRedo (handed back by the ring decoder)
     const uint64_t* bitmap;      // token bitmaps of pass 1 (lz4mi_token_map_kernel): replace the speculative parse
     const uint32_t* chunk_base;  // first bitmap chunk of each block
 };
 
-constexpr int32_t kStatusF1 = -10;   // internal: block must be decoded by the serial reference-exact kernel
 constexpr int32_t kStatusRedo = -11; // internal: the two-pass ring decoder hands the block to the single-pass kernel
 
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream);
-// Re-decode, one block per workgroup, every block whose status is kStatusF1.
-extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream);
 
 // Two-pass ring decoder (lz4mi_decompress_ring.hip).
 extern "C" hipError_t lz4mi_launch_ring_plan(const uint32_t* in_len, const uint32_t* out_cap, uint32_t min_ratio,

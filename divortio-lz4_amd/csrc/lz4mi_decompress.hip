@@ -801,6 +801,61 @@ __device__ __forceinline__ uint32_t f1_changes(const Ctx& c, int32_t ms, int32_t
     return 0;
 }
 
+// Reference-exact fix-up of one chunk (LZ4MI_JS_EXACT) whose matches include a
+// double-copy-tail rewrite that changes bytes (f1_changes == 1): the chunk was written
+// with spec semantics; replay its matches in order with the reference's semantics.
+// Literal bytes never change. Everything before the first rewritten position `lo` is
+// already final, so a match is copied again only if its source reaches past `lo`
+// (periodic copy: its source bytes before its start are final when it runs), and every
+// rewrite is applied (blockDecompress.js:219-250: out[p] = out[p - off] for
+// p in [ms + ml - 8, ms), after the copy). Later chunks then read the fixed output.
+__device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t nseq, bool cut, int64_t cut_ms,
+                         int32_t coff, int32_t cml) {
+    int64_t lo = INT64_MAX;
+    const uint32_t n = nseq + (cut ? 1u : 0u);
+    for (uint32_t k = 0; k < n; ++k) {
+        int64_t ms;
+        int32_t off, ml;
+        if (k < nseq) {
+            const SeqInfo q = seq_info(S, k);
+            ms = (int64_t)S.t_out[k] + q.ll;
+            off = q.off;
+            ml = q.ml;
+        } else {
+            ms = cut_ms;
+            off = coff;
+            ml = cml;
+        }
+        if (ml == 0) continue;
+        const bool internal = c.out_off + ms - off >= 0;   // the reference's non-dictionary branch
+        if (ms - off + ml > lo) {
+            if (internal) {
+                for (int32_t t = lane; t < ml; t += kWave) {
+                    const int64_t d = ms + t;
+                    const int64_t s = ms - off + (off < ml ? t % off : t);
+                    const uint32_t v = ld_nt_u8(c.dst + s);
+                    if (d < c.cap) c.dst[d] = (uint8_t)v;
+                }
+            } else if (lane == 0) {   // spills from the dictionary into the output: in order, byte by byte
+                for (int32_t t = 0; t < ml; ++t) {
+                    const uint32_t v = hist_byte(c, ms - off + t);
+                    if (ms + t < c.cap) c.dst[ms + t] = (uint8_t)v;
+                }
+            }
+            wait_vmem();
+        }
+        if (internal && off >= 8 && ml < 8) {
+            const int64_t p = ms + ml - 8 + lane;
+            const bool mine = lane < 8 - ml && c.out_off + p >= 0 && p < c.cap;
+            const uint32_t v = mine ? (c.out_off + p - off >= 0 ? ld_nt_u8(c.dst + p - off) : 0u) : 0u;
+            if (mine) c.dst[p] = (uint8_t)v;
+            const int64_t p0 = ms + ml - 8;
+            if (p0 < lo) lo = p0;
+            wait_vmem();
+        }
+    }
+}
+
 // BM: the chunk's token starts come from pass 1's bitmap (lz4mi_decompress_ring.hip)
 // instead of the next-token table / jump tables / speculative walks; chunks are then
 // the fixed 1 KiB chunks of the bitmap, staged from their base.
@@ -1258,7 +1313,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             }
             if (cut && lane == 0) dv |= f1_changes(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
             if (__ballot(dv & 2u)) { status = -9; break; }
-            if (__ballot(dv)) { status = kStatusF1; break; }
+            if (__ballot(dv)) f1_fixup(c, S, lane, nseq, cut, (int64_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
         }
         c.O = tab_hi;
         if (cut) {
@@ -1299,15 +1354,14 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
                                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                               const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
                                               int32_t* status, uint32_t nblocks, int mode, hipStream_t stream) {
-    // mode 0: LZ4 spec; 1: reference-exact serial kernel; 2: spec kernel + serial redo of F1 blocks
+    // mode 0: LZ4 spec; 1: reference-exact serial kernel; 2: spec kernel with the in-chunk
+    // reference-exact fix-up of every chunk a double-copy-tail rewrite changes (f1_fixup)
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, mode == 2 ? 1 : 0};
     if (nblocks == 0) return hipSuccess;
     if (mode == 1) return lz4mi_launch_decompress_serial(a, stream);
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || mode != 2) return e;
-    return lz4mi_launch_decompress_redo(a, stream);
+    return hipGetLastError();
 }
 
 // Re-decode every block the two-pass ring decoder handed back (status kStatusRedo),

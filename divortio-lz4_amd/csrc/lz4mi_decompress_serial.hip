@@ -11,12 +11,7 @@
 
 namespace lz4mi {
 
-// isolated: the block is one of a batch decoded in parallel (the F1 redo of LZ4MI_JS_EXACT):
-// bytes before its own output may still be in flight, so a read or rewrite there is
-// reported (LZ4MI_ERR_CROSS_BLOCK) and the caller decodes the block alone, in order.
-constexpr int32_t kCrossBlock = -9;   // LZ4MI_ERR_CROSS_BLOCK
-
-__device__ void decode_block_jscompat(const DecArgs& a, uint32_t b, bool isolated) {
+__device__ void decode_block_jscompat(const DecArgs& a, uint32_t b) {
     const uint8_t* in = a.in + a.in_off[b];
     const int64_t iend = a.in_len[b];
     uint8_t* out = a.out;                       // absolute positions
@@ -56,10 +51,6 @@ __device__ void decode_block_jscompat(const DecArgs& a, uint32_t b, bool isolate
             continue;
         }
         int64_t start = op;
-        if (isolated && (from < oo || (off >= 8 && ml < 8 && start + ml - 8 - (int64_t)off < oo))) {
-            st = kCrossBlock;
-            break;
-        }
         for (int64_t k = 0; k < ml; ++k) {
             int64_t r = op - off;
             uint8_t v = r < olen ? out[r] : 0;
@@ -80,23 +71,13 @@ __device__ void decode_block_jscompat(const DecArgs& a, uint32_t b, bool isolate
 
 __global__ __launch_bounds__(64) void lz4mi_decompress_jscompat_kernel(DecArgs a) {
     if (threadIdx.x != 0) return;
-    for (uint32_t b = 0; b < a.nblocks; ++b) decode_block_jscompat(a, b, false);
+    for (uint32_t b = 0; b < a.nblocks; ++b) decode_block_jscompat(a, b);
 }
 
-__global__ __launch_bounds__(64) void lz4mi_decompress_redo_kernel(DecArgs a) {
-    const uint32_t b = blockIdx.x;
-    if (threadIdx.x != 0 || b >= a.nblocks || a.status[b] != kStatusF1) return;
-    decode_block_jscompat(a, b, a.isolate != 0);
-}
 
 }  // namespace lz4mi
 
 extern "C" hipError_t lz4mi_launch_decompress_serial(const lz4mi::DecArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_jscompat_kernel, dim3(1), dim3(64), 0, stream, a);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t lz4mi_launch_decompress_redo(const lz4mi::DecArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_redo_kernel, dim3(a.nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }

@@ -58,9 +58,10 @@ extern "C" {
                                     double-copy-tail rewrite. Default: LZ4 spec. */
 #define LZ4MI_XXH_STANDARD 0x4u  /* spec XXH32 lane convergence instead of the reference's variant */
 #define LZ4MI_JS_EXACT 0x8u      /* reference-exact result at spec-decoder speed: blocks are decoded by the
-                                    parallel spec kernel, which flags every block where the reference's
-                                    double-copy-tail rewrite (F1) would change a byte; only those blocks are
-                                    decoded again by the serial reference-exact kernel. */
+                                    parallel spec kernel, which checks every 1 KiB chunk for a reference
+                                    double-copy-tail rewrite (F1) that would change a byte and, only in such
+                                    a chunk, replays the chunk's matches with the reference's semantics
+                                    before going on (cost proportional to the affected chunks). */
 
 #define LZ4MI_XXH_LEN64 0x10u    /* streaming XXH32: keep the 64-bit total length (streams over 2 GiB);
                                     default: the reference class's `(totalLen + len) | 0` */

@@ -230,3 +230,24 @@ def test_ring_decoder_bitmap_overflow_falls_back_exactly(monkeypatch):
     assert (st == 0).all()
     for s, o in zip(srcs, outs):
         assert np.array_equal(s, o)
+
+
+@pytest.mark.parametrize("kind", ["copy", "runs", "text", "tiles216"])
+def test_js_exact_fixup_matches_reference_decoder(kind):
+    """LZ4MI_JS_EXACT (the JS layer's default): the parallel kernel's in-chunk replay of the
+    reference's double-copy-tail rewrites (F1) gives the reference decoder's bytes on
+    F1-heavy data (copy: ~19% of sequences), batched and per block."""
+    sizes = [1 << 20, 4 << 20, 300001]
+    srcs = [O.generate(kind, 70 + k, n) for k, n in enumerate(sizes)]
+    comps = [O.compress_block_bytes(s) for s in srcs]
+    st, outs, lens = lz4mi.decompress_blocks(comps, sizes, js_exact=True)
+    for k, (s, c) in enumerate(zip(srcs, comps)):
+        est, ew, eo = O.decompress_block(c, sizes[k], js_compat=True)
+        assert est == 0
+        if st[k] == lz4mi.ERR_CROSS_BLOCK:       # its first rewrite reaches the previous block's bytes
+            out = np.zeros(sizes[k], dtype=np.uint8)
+            w = lz4mi.decompress_raw(c, 0, c.size, out, 0, js_exact=True)
+            assert w == ew and np.array_equal(out, eo[:sizes[k]]), (kind, k)
+            continue
+        assert st[k] == 0 and lens[k] == ew, (kind, k)
+        assert np.array_equal(outs[k], eo[:sizes[k]]), (kind, k)
