@@ -641,10 +641,6 @@ struct GtShared {
     uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
 };
 
-// HEAD_LDST: the head probe reads its slot with a plain (L1-bypassing) load and writes it
-// back with a plain store instead of one atomic exchange (experiment: atomics execute at
-// the memory side).
-template <bool HEAD_LDST>
 __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, int lane) {
     const int32_t n = j.len;
     const int32_t mflimit = n - 12, matchlimit = n - 5;
@@ -671,14 +667,8 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         }
         const uint32_t h0 = (seq0 * kP1) >> 18;
         int32_t old = 0;
-        if (HEAD_LDST) {
-            old = __builtin_nontemporal_load(&T[h0]);
-            old = (int32_t)uniform((uint32_t)old);
-            if (lane == 0) T[h0] = i + 1;
-        } else {
-            if (lane == 0) old = atomicExch(&T[h0], i + 1);
-            old = (int32_t)uniform((uint32_t)old);
-        }
+        if (lane == 0) old = atomicExch(&T[h0], i + 1);
+        old = (int32_t)uniform((uint32_t)old);
         int32_t cand0 = old - 1;
         if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
         uint32_t aw = 0, bw = 0;
@@ -725,7 +715,6 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
             pv = false;
         }
         // ---- the probe at i missed (and inserted itself): the next probes of the miss chain as a batch
-        if (HEAD_LDST) wait_vmem();   // the head's store is complete before the batch reads the table
         i += (int32_t)(c >> 6);
         c += 1;
         if (i >= mflimit) break;
@@ -793,7 +782,6 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
     return o.op;
 }
 
-template <bool HEAD_LDST>
 __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, int32_t* tables) {
     __shared__ GtShared F;
     const uint32_t b = blockIdx.x;
@@ -807,7 +795,7 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, in
     j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
     j.dst_pos = 0;
     j.table = nullptr;
-    const int64_t r = compress_block_gt<HEAD_LDST>(j, F, tables + (size_t)b * 16384, threadIdx.x);
+    const int64_t r = compress_block_gt(j, F, tables + (size_t)b * 16384, threadIdx.x);
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
@@ -835,11 +823,7 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
         hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
         return hipGetLastError();
     }
-    if (enc && enc[0] == 'x') {   // experiment: plain load + store head probe
-        hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel<true>, dim3(nblocks), dim3(64), 0, stream, a, tables);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel<false>, dim3(nblocks), dim3(64), 0, stream, a, tables);
+    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
     return hipGetLastError();
 }
 
