@@ -38,6 +38,11 @@ extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int3
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
                                          uint32_t, int, uint8_t*, const uint64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_generate(uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
+extern "C" hipError_t lz4mi_launch_frame_scan(const uint8_t*, uint64_t, uint32_t, uint64_t*, uint32_t*, uint64_t*,
+                                              uint32_t*, uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint32_t*,
+                                              int64_t*, hipStream_t);
+extern "C" hipError_t lz4mi_launch_frame_stored(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*,
+                                                const uint64_t*, uint8_t*, uint64_t, uint32_t, hipStream_t);
 
 namespace {
 
@@ -72,6 +77,7 @@ struct StreamCtx {
     Scratch chunk_base;   // two-pass decoder: first bitmap chunk of each block (device plan)
     Scratch bitmap;       // token bitmaps, 128 B per 1 KiB compressed chunk
     Scratch frame_meta;   // block-checksum payload offsets / lengths of frame_pack
+    Scratch scan;         // frame_decompress: block lists of the device frame walk
     uint64_t bitmap_chunks = 0;
     uint32_t* needed = nullptr;   // host-mapped: chunks the last plan wanted (read lazily)
     void release() {
@@ -79,6 +85,7 @@ struct StreamCtx {
         chunk_base.release();
         bitmap.release();
         frame_meta.release();
+        scan.release();
         if (needed) (void)hipHostFree(needed);
         needed = nullptr;
         bitmap_chunks = 0;
@@ -638,6 +645,104 @@ int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint
     LZ4MI_TRY(lz4mi_launch_frame_pack(raw, raw_off, raw_len, comp, comp_off, comp_len, frame, rec_off, nblocks,
                                       pay_off, sum_off, pay_len, s));
     LZ4MI_TRY(lz4mi_launch_xxh32(frame, pay_off, pay_len, 0, nullptr, nblocks, 1, frame, sum_off, s));
+    return LZ4MI_OK;
+}
+
+int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out, uint64_t out_cap, int64_t* info,
+                               uint32_t flags, void* stream) {
+    int32_t st = ensure_init();
+    if (st) return st;
+    if (!(flags & LZ4MI_DEVICE_PTRS) || !info || (flags & LZ4MI_JS_COMPAT)) return LZ4MI_ERR_ARG;
+    for (int k = 0; k < 8; ++k) info[k] = 0;
+    hipStream_t s = pick_stream(stream);
+    const int mode = (flags & LZ4MI_JS_EXACT) ? 2 : 0;
+    // the header (<= 19 bytes) first: the content size bounds the number of blocks of the reference's layout
+    uint8_t h[19] = {0};
+    LZ4MI_TRY(hipMemcpyAsync(h, frame, std::min<uint64_t>(len, 19), hipMemcpyDeviceToHost, s));
+    LZ4MI_TRY(hipStreamSynchronize(s));
+    const uint64_t size = (len >= 14 && (h[4] & 0x08)) ? (uint64_t)le32(h + 6) | ((uint64_t)le32(h + 10) << 32) : 0;
+    const uint32_t id = len > 5 ? (h[5] >> 4) & 7 : 7;
+    const uint64_t bmax = id == 4 ? 65536 : id == 5 ? 262144 : id == 6 ? 1048576 : 4194304;
+    const uint64_t cap_blocks = size / bmax + 2;
+    if (cap_blocks > 0xFFFFFFF0ull) return LZ4MI_ERR_ARG;
+    StreamCtx* c = stream_ctx(s);
+    const size_t per = 8 + 4 + 8 + 4 + 4;   // compressed lists (in_off, in_len, out_off, out_cap, idx)
+    const size_t per_s = 8 + 4 + 8 + 4;     // stored lists (in_off, len, out_off, idx)
+    const size_t meta = cap_blocks * (per + per_s + 4 + 4) + 64 + 64;   // + out_len, status
+    LZ4MI_TRY(c->scan.ensure(meta, s));
+    uint8_t* m = c->scan.as<uint8_t>();
+    int64_t* d_info = (int64_t*)m;
+    uint64_t* c_in_off = (uint64_t*)(m + 64);
+    uint64_t* c_out_off = c_in_off + cap_blocks;
+    uint64_t* s_in_off = c_out_off + cap_blocks;
+    uint64_t* s_out_off = s_in_off + cap_blocks;
+    uint32_t* c_in_len = (uint32_t*)(s_out_off + cap_blocks);
+    uint32_t* c_out_cap = c_in_len + cap_blocks;
+    uint32_t* c_idx = c_out_cap + cap_blocks;
+    uint32_t* s_len = c_idx + cap_blocks;
+    uint32_t* s_idx = s_len + cap_blocks;
+    uint32_t* d_out_len = s_idx + cap_blocks;
+    int32_t* d_status = (int32_t*)(d_out_len + cap_blocks);
+    LZ4MI_TRY(lz4mi_launch_frame_scan(frame, len, (uint32_t)cap_blocks, c_in_off, c_in_len, c_out_off, c_out_cap,
+                                      s_in_off, s_len, s_out_off, c_idx, s_idx, d_info, s));
+    int64_t hi[8];
+    LZ4MI_TRY(hipMemcpyAsync(hi, d_info, sizeof hi, hipMemcpyDeviceToHost, s));
+    LZ4MI_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < 8; ++k) info[k] = hi[k];
+    if (hi[0]) return LZ4MI_OK;                        // magic / version: info[0] holds the reference's error
+    if (hi[2] <= 0 || hi[7]) return LZ4MI_ERR_ARG;     // no content size, or not the reference's layout: host path
+    if ((uint64_t)hi[2] > out_cap) return LZ4MI_ERR_ARG;
+    const uint32_t nc = (uint32_t)hi[3], ns = (uint32_t)hi[4];
+    // stored blocks, then every compressed block in one batch (spec or reference-exact)
+    LZ4MI_TRY(lz4mi_launch_frame_stored(frame, len, s_in_off, s_len, s_out_off, out, (uint64_t)hi[2], ns, s));
+    if (nc) LZ4MI_TRY(decode_launch(frame, c_in_off, c_in_len, out, c_out_off, c_out_cap, nullptr, 0, d_out_len,
+                                    d_status, nc, mode, s));
+    std::vector<uint32_t> olen(nc), cap(nc), cidx(nc), slen(ns), sidx(ns);
+    std::vector<int32_t> stat(nc);
+    std::vector<uint64_t> soff(ns), ooff(nc), ioff(nc);
+    if (nc) {
+        LZ4MI_TRY(hipMemcpyAsync(olen.data(), d_out_len, 4ull * nc, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(stat.data(), d_status, 4ull * nc, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(cap.data(), c_out_cap, 4ull * nc, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(cidx.data(), c_idx, 4ull * nc, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(ooff.data(), c_out_off, 8ull * nc, hipMemcpyDeviceToHost, s));
+    }
+    if (ns) {
+        LZ4MI_TRY(hipMemcpyAsync(slen.data(), s_len, 4ull * ns, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(sidx.data(), s_idx, 4ull * ns, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(soff.data(), s_out_off, 8ull * ns, hipMemcpyDeviceToHost, s));
+    }
+    LZ4MI_TRY(hipStreamSynchronize(s));
+    // blocks that read earlier blocks' output (dependent frames, or an F1 rewrite at a block start):
+    // every block before them is final now; decode each alone, in order
+    for (uint32_t k = 0; k < nc; ++k) {
+        if (stat[k] != LZ4MI_ERR_CROSS_BLOCK) continue;
+        LZ4MI_TRY(decode_launch(frame, c_in_off + k, c_in_len + k, out, c_out_off + k, c_out_cap + k, nullptr, 0,
+                                d_out_len + k, d_status + k, 1, mode, s));
+        LZ4MI_TRY(hipMemcpyAsync(&olen[k], d_out_len + k, 4, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipMemcpyAsync(&stat[k], d_status + k, 4, hipMemcpyDeviceToHost, s));
+        LZ4MI_TRY(hipStreamSynchronize(s));
+    }
+    // the reference's first error in block order; every compressed block but the frame's last must fill
+    // block_max (the layout the output positions assumed), else the host path decodes the frame
+    const uint64_t size_v = (uint64_t)hi[2];
+    uint32_t first = UINT32_MAX;
+    int32_t first_st = 0;
+    uint64_t written = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+        // the reference's capacity is the whole result, not the block's slot: a block that overran
+        // its slot is not the reference encoder's layout (the host path decodes such a frame)
+        if (stat[k] == LZ4MI_ERR_OUTPUT_TOO_SMALL && ooff[k] + cap[k] < size_v) return LZ4MI_ERR_ARG;
+        if (stat[k] && cidx[k] < first) { first = cidx[k]; first_st = stat[k]; }
+        if (!stat[k]) written = std::max<uint64_t>(written, ooff[k] + olen[k]);
+        if (!stat[k] && olen[k] != cap[k] && cidx[k] != nc + ns - 1) return LZ4MI_ERR_ARG;
+    }
+    for (uint32_t k = 0; k < ns; ++k) {
+        if (soff[k] + slen[k] > size_v && sidx[k] < first) { first = sidx[k]; first_st = LZ4MI_ERR_RANGE; }
+        written = std::max<uint64_t>(written, std::min<uint64_t>(soff[k] + slen[k], size_v));
+    }
+    info[0] = first_st;
+    info[3] = (int64_t)written;
     return LZ4MI_OK;
 }
 

@@ -59,7 +59,133 @@ __global__ __launch_bounds__(64) void lz4mi_frame_pack_kernel(const uint8_t* raw
     }
 }
 
+// ---------------------------------------------------------------------------
+// Decode side: the frame's header and block walk on the device (the reference's
+// decompressBuffer, src/buffer/bufferDecompress.js:56-92 header, :133-192 block loop).
+// One lane walks the size words (each record's position depends on the previous
+// size); compressed and stored blocks go to two lists. Output positions assume the
+// reference encoder's layout (every block but the last fills block_max bytes; the
+// caller checks the decoded lengths, as the JS layer's batch path does).
+// info[0] status (0, LZ4MI_ERR_MAGIC -5, LZ4MI_ERR_VERSION -6), [1] FLG, [2] content size,
+// [3] compressed blocks, [4] stored blocks, [5] position after the EndMark (content
+// checksum), [6] block_max (BD), [7] 1 if the walk ran past the frame or the lists' capacity.
+__global__ __launch_bounds__(64) void lz4mi_frame_scan_kernel(const uint8_t* f, uint64_t len, uint32_t cap_blocks,
+                                                              uint64_t* c_in_off, uint32_t* c_in_len,
+                                                              uint64_t* c_out_off, uint32_t* c_out_cap,
+                                                              uint64_t* s_in_off, uint32_t* s_len, uint64_t* s_out_off,
+                                                              uint32_t* c_idx, uint32_t* s_idx, int64_t* info) {
+    if (threadIdx.x != 0) return;
+    auto rd = [&](uint64_t p) -> uint32_t {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) v |= (p + k < len ? (uint32_t)f[p + k] : 0u) << (8 * k);
+        return v;
+    };
+    int64_t st = 0, flg = 0, size = 0, nc = 0, ns = 0, overflow = 0;
+    uint64_t pos = 0;
+    int64_t bmax = 4194304;
+    if (len < 4 || rd(0) != 0x184D2204u) {
+        st = -5;
+    } else {
+        flg = len > 4 ? f[4] : 0;
+        if (((flg & 0xC0) >> 6) != 1) {
+            st = -6;
+        } else {
+            const uint32_t bd = len > 5 ? f[5] : 0;
+            const uint32_t id = (bd >> 4) & 7;
+            bmax = id == 4 ? 65536 : id == 5 ? 262144 : id == 6 ? 1048576 : 4194304;
+            pos = 6;
+            if (flg & 0x08) {
+                size = (int64_t)((uint64_t)rd(pos) | ((uint64_t)rd(pos + 4) << 32));
+                pos += 8;
+            }
+            if (flg & 0x01) pos += 4;
+            pos += 1;
+            uint64_t op = 0;
+            while (pos < len) {
+                const uint32_t bs = rd(pos);
+                pos += 4;
+                if (bs == 0) break;
+                const uint32_t n = bs & 0x7FFFFFFFu;
+                if (nc + ns >= (int64_t)cap_blocks) { overflow = 1; break; }
+                if (bs & 0x80000000u) {
+                    s_in_off[ns] = pos;
+                    s_len[ns] = n;
+                    s_out_off[ns] = op;
+                    s_idx[ns] = (uint32_t)(nc + ns);
+                    ++ns;
+                    op += n;               // the reference advances by the declared size
+                } else {
+                    c_in_off[nc] = pos;
+                    c_in_len[nc] = n;
+                    c_out_off[nc] = op;
+                    const int64_t left = size - (int64_t)op;
+                    c_out_cap[nc] = (uint32_t)(left < 0 ? 0 : (left < bmax ? left : bmax));
+                    c_idx[nc] = (uint32_t)(nc + ns);
+                    ++nc;
+                    op += (uint64_t)bmax;
+                }
+                pos += n + ((flg & 0x10) ? 4 : 0);
+            }
+            if (pos > len) overflow = 1;
+        }
+    }
+    info[0] = st; info[1] = flg; info[2] = size; info[3] = nc; info[4] = ns;
+    info[5] = (int64_t)pos; info[6] = bmax; info[7] = overflow;
+}
+
+// Stored blocks' bytes into the output (one wave per stored block; clipped at `cap`
+// like the reference's result.set would throw past it: the caller checks first).
+__global__ __launch_bounds__(64) void lz4mi_frame_stored_kernel(const uint8_t* f, uint64_t len, const uint64_t* s_in_off,
+                                                                const uint32_t* s_len, const uint64_t* s_out_off,
+                                                                uint8_t* out, uint64_t cap, uint32_t ns) {
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (b >= ns) return;
+    const uint64_t src = s_in_off[b], dst = s_out_off[b];
+    uint64_t n = s_len[b];
+    if (src + n > len) n = src < len ? len - src : 0;      // subarray() clips at the frame end
+    if (dst + n > cap) n = dst < cap ? cap - dst : 0;
+    if (n < 16) {
+        if ((uint64_t)lane < n) out[dst + lane] = f[src + lane];
+        return;
+    }
+    const uint64_t np = (n + 15) / 16;   // 16-byte pieces, the last one overlapping its predecessor
+    for (uint64_t p0 = 0; p0 < np; p0 += 4 * kWave) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t p = p0 + lane + kWave * u;
+            const uint64_t d = 16 * p < n - 16 ? 16 * p : n - 16;
+            if (p < np) __builtin_memcpy(&v[u], f + src + d, 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t p = p0 + lane + kWave * u;
+            const uint64_t d = 16 * p < n - 16 ? 16 * p : n - 16;
+            if (p < np) __builtin_memcpy(out + dst + d, &v[u], 16);
+        }
+    }
+}
+
 }  // namespace lz4mi
+
+extern "C" hipError_t lz4mi_launch_frame_scan(const uint8_t* f, uint64_t len, uint32_t cap_blocks, uint64_t* c_in_off,
+                                              uint32_t* c_in_len, uint64_t* c_out_off, uint32_t* c_out_cap,
+                                              uint64_t* s_in_off, uint32_t* s_len, uint64_t* s_out_off, uint32_t* c_idx,
+                                              uint32_t* s_idx, int64_t* info, hipStream_t stream) {
+    hipLaunchKernelGGL(lz4mi::lz4mi_frame_scan_kernel, dim3(1), dim3(64), 0, stream, f, len, cap_blocks, c_in_off,
+                       c_in_len, c_out_off, c_out_cap, s_in_off, s_len, s_out_off, c_idx, s_idx, info);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t lz4mi_launch_frame_stored(const uint8_t* f, uint64_t len, const uint64_t* s_in_off,
+                                                const uint32_t* s_len, const uint64_t* s_out_off, uint8_t* out,
+                                                uint64_t cap, uint32_t ns, hipStream_t stream) {
+    if (ns == 0) return hipSuccess;
+    hipLaunchKernelGGL(lz4mi::lz4mi_frame_stored_kernel, dim3(ns), dim3(64), 0, stream, f, len, s_in_off, s_len,
+                       s_out_off, out, cap, ns);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len,
                                               const uint8_t* comp, const uint64_t* comp_off, const uint32_t* comp_len,

@@ -37,7 +37,8 @@ GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GE
 EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_version",
            "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
-           "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest")
+           "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
+           "lz4mi_frame_decompress")
 
 
 class Lz4miError(RuntimeError):
@@ -90,6 +91,8 @@ def lib():
         L.lz4mi_xxh32_blocks.argtypes = [_vp, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
         L.lz4mi_frame_pack.restype = ctypes.c_int32
         L.lz4mi_frame_pack.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
+        L.lz4mi_frame_decompress.restype = ctypes.c_int32
+        L.lz4mi_frame_decompress.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
         L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, _vp]
@@ -283,6 +286,16 @@ def compress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, ou
 def xxh32_blocks_dev(in_ptr, off_ptr, len_ptr, hashes_ptr, nblocks, seed=0, stream=0, standard=False):
     _check(lib().lz4mi_xxh32_blocks(in_ptr, off_ptr, len_ptr, seed & 0xFFFFFFFF, hashes_ptr, nblocks,
                                     DEVICE_PTRS | (XXH_STANDARD if standard else 0), stream or None))
+
+
+def frame_decompress_dev(frame_ptr, frame_len, out_ptr, out_cap, stream=0, js_exact=False):
+    """Decode a device-resident LZ4 frame into out (device pointers): returns the info dict
+    (include/lz4mi.h lz4mi_frame_decompress); raises if the frame needs the host path."""
+    info = np.zeros(8, dtype=np.int64)
+    _check(lib().lz4mi_frame_decompress(frame_ptr, frame_len, out_ptr, out_cap, info.ctypes.data,
+                                        DEVICE_PTRS | (JS_EXACT if js_exact else 0), stream or None))
+    keys = ("status", "flg", "content_size", "written", "stored_blocks", "checksum_pos", "block_max", "overflow")
+    return dict(zip(keys, (int(x) for x in info)))
 
 
 def generate_blocks_dev(out_ptr, kind, seed0, block_size, nblocks, stream=0):

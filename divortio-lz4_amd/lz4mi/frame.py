@@ -262,6 +262,36 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     return out
 
 
+def decompress_frame_device(frame, js_exact=False, verify_checksum=True, stream=None):
+    """Decode a device-resident frame (1-D uint8 CUDA tensor) on its GPU: the header and the
+    block walk run on the device (lz4mi_frame_decompress), stored blocks are copied and the
+    compressed ones decoded in one batch; the content checksum (FLG 0x04) is verified on the
+    host, streamed piece by piece. Returns the content as a uint8 CUDA tensor. Raises
+    lz4mi.Lz4miError with the reference's message for the frame's first error."""
+    import torch
+    import lz4mi
+    s = stream if stream is not None else torch.cuda.current_stream()
+    head = frame[:19].cpu().numpy()
+    if head.size < 4 or int.from_bytes(head[:4].tobytes(), "little") != 0x184D2204:
+        raise lz4mi.Lz4miError(lz4mi.ERR_MAGIC)
+    size = int.from_bytes(head[6:14].tobytes(), "little") if head.size >= 14 and head[4] & 0x08 else 0
+    out = torch.empty(max(1, size), dtype=torch.uint8, device=frame.device)
+    info = lz4mi.frame_decompress_dev(frame.data_ptr(), frame.numel(), out.data_ptr(), size, s.cuda_stream,
+                                      js_exact=js_exact)
+    if info["status"]:
+        raise lz4mi.Lz4miError(info["status"])
+    out = out[:info["written"]]
+    if verify_checksum and info["flg"] & 0x04:
+        pos = info["checksum_pos"]
+        want = int.from_bytes(frame[pos:pos + 4].cpu().numpy().tobytes(), "little")
+        w = _ChecksumWorker()
+        for p in range(0, out.numel(), CHECKSUM_PIECE):
+            w.feed(out[p:p + CHECKSUM_PIECE].cpu().numpy())
+        if w.digest() != want:
+            raise lz4mi.Lz4miError(lz4mi.ERR_CHECKSUM)
+    return out
+
+
 def _gpu_decode(comp, block_max):
     import lz4mi
     payloads = [c for c, stored in comp if not stored]

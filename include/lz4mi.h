@@ -183,6 +183,27 @@ int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint
                          uint32_t nblocks, uint32_t flags, void* stream);
 
 /*
+ * LZ4 frame DECOMPRESS of a frame in device memory (content size present).
+ * Replaces decompressBuffer src/buffer/bufferDecompress.js:51-220 ("direct write" strategy, :97):
+ * the header and the size words are walked on the device (one lane: each record's position
+ * depends on the previous size), stored blocks are copied (:146-148), and the compressed blocks
+ * are decoded in one batch at the output positions of the reference encoder's layout; a block
+ * that reads an earlier block's output (dependent frames) is then decoded alone, in order.
+ * out: device buffer of out_cap >= content-size bytes. info (host, 8 x int64): [0] the reference's
+ * error for the frame (first failing block in block order: LZ4MI_ERR_* of the block decoder,
+ * LZ4MI_ERR_RANGE for a stored block past the content size, LZ4MI_ERR_MAGIC / _VERSION for the
+ * header) or 0; [1] FLG; [2] content size; [3] bytes written; [4] stored blocks; [5] position
+ * of the content checksum (after the EndMark) when FLG has 0x04; [6] block max size (BD).
+ * The content checksum (one serial XXH32 chain) is the caller's to verify.
+ * flags: LZ4MI_DEVICE_PTRS (required) | LZ4MI_JS_EXACT (reference-exact; default LZ4 spec).
+ * Synchronous (reads the header and the block lists back). Returns LZ4MI_ERR_ARG for frames
+ * this path does not take (no content size, a block layout other than the reference encoder's,
+ * out_cap too small): decode those with the host-buffer path block by block.
+ */
+int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out, uint64_t out_cap, int64_t* info,
+                               uint32_t flags, void* stream);
+
+/*
  * Synthetic input generator (bench/test support, not a reference interface):
  * block b = generator `kind` with seed seed0 + b, block_size bytes each,
  * written to out[b * block_size ..] (device pointer, async on stream).

@@ -251,3 +251,35 @@ def test_js_exact_fixup_matches_reference_decoder(kind):
             continue
         assert st[k] == 0 and lens[k] == ew, (kind, k)
         assert np.array_equal(outs[k], eo[:sizes[k]]), (kind, k)
+
+
+def test_frame_decompress_on_device_matches_reference():
+    """lz4mi_frame_decompress: header + size-word walk on the device, stored blocks copied,
+    compressed blocks batched (dependent blocks re-decoded in order); == the oracle's frame
+    decode for independent/dependent frames, with stored blocks, block checksums and the
+    content checksum; the reference's errors for a bad magic and a corrupted checksum."""
+    from lz4mi import frame as F
+    data = np.concatenate([O.generate("tiles216", 31, 900000), O.generate("random", 32, 300000),
+                           O.generate("text", 33, 500000), O.generate("repetitive", 34, 77777)])
+    cases = [(65536, True, True, False), (262144, False, True, False), (1048576, True, False, True),
+             (4194304, True, True, False), (65536, False, False, True)]
+    for bs, indep, cs, bcs in cases:
+        f = O.compress_frame(data, None, bs, indep, cs, True, block_checksum=bcs)
+        st, ref_spec = O.decompress_frame(f, verify_checksum=False)
+        assert st == 0 and np.array_equal(ref_spec, data)
+        dev = torch.from_numpy(f.copy()).cuda()
+        got = F.decompress_frame_device(dev, js_exact=False, verify_checksum=cs)
+        assert np.array_equal(got.cpu().numpy(), data), (bs, indep, cs, bcs)
+        # reference-exact: the oracle's reference decode (F1 on the text part); checksum as the reference checks it
+        est, eref = O.decompress_frame(f, verify_checksum=cs, js_compat=True)
+        if est == 0:
+            got = F.decompress_frame_device(dev, js_exact=True, verify_checksum=cs)
+            assert np.array_equal(got.cpu().numpy(), eref), (bs, indep, cs, bcs)
+        else:
+            with pytest.raises(lz4mi.Lz4miError) as ei:
+                F.decompress_frame_device(dev, js_exact=True, verify_checksum=cs)
+            assert ei.value.status == est
+    bad = torch.from_numpy(np.frombuffer(bytes(range(6)), dtype=np.uint8).copy()).cuda()
+    with pytest.raises(lz4mi.Lz4miError) as ei:
+        F.decompress_frame_device(bad)
+    assert str(ei.value) == "LZ4: Invalid Magic Number"
