@@ -188,7 +188,18 @@ def frame_assembly(torch, dist, lz4mi, batch, stream, stream_obj, steps, world):
     ok = True
     if got[0] is not None:
         ok = bool(torch.equal(got[0][:4], records[:4])) and got[0].numel() == int(tot.item())
+    # the frame's content checksum is one serial XXH32 chain over all raw bytes: its host
+    # rate (streaming state, 64-bit length) on a 256 MiB sample of this rank's raw blocks
+    sample = batch.raw[:min(batch.n, 64) * BLOCK].cpu().numpy()
+    h = lz4mi.XXHash32(0, len64=True)
+    t0 = time.perf_counter()
+    h.update(sample)
+    h.digest()
+    xxh_gbps = sample.size / (time.perf_counter() - t0) / 1e9
     return {"record_GBps": round(int(tot.item()) * steps / wall / 1e9, 2),
+            "content_checksum_host_GBps": round(xxh_gbps, 2),
+            "content_checksum_note": "one host core (the chain is serial); the sharded-frame path "
+                                     "(lz4mi.frame) overlaps it with the record gather",
             "note": "frame record bytes (size words + payloads) packed and gathered per second",
             "ms_per_step": round(wall / steps * 1e3, 3), "record_bytes": int(tot.item()),
             "collective": "all_gather(sizes) + send/irecv to rank 0" if dist is not None else None,

@@ -24,8 +24,10 @@ __device__ __forceinline__ uint32_t load_le32(const uint8_t* p, bool aligned) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// hashes[buf] = digest; or, with `dst` set, the digest stored little-endian at dst + dst_off[buf]
-// (frame block checksums written after their payloads).
+// hashes[buf] = digest; or (TO_FRAME) the digest stored little-endian at dst + dst_off[buf]
+// (frame block checksums written after their payloads). Two instantiations, so the plain
+// batch kernel keeps its register allocation.
+template <bool TO_FRAME>
 __global__ __launch_bounds__(256) void lz4mi_xxh32_kernel(const uint8_t* in, const uint64_t* off, const uint32_t* len,
                                                           uint32_t seed, uint32_t* hashes, uint32_t n, int standard,
                                                           uint8_t* dst, const uint64_t* dst_off) {
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(256) void lz4mi_xxh32_kernel(const uint8_t* in, con
     for (; pos + 4 <= L; pos += 4) h = rotl(h + load_le32(p + pos, false) * P3, 17) * P4;
     for (; pos < L; ++pos) h = rotl(h + p[pos] * P5, 11) * P1;
     h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
-    if (dst) {
+    if (TO_FRAME) {
         uint8_t* q8 = dst + dst_off[buf];
         for (int k = 0; k < 4; ++k) q8[k] = (uint8_t)(h >> (8 * k));
     } else {
@@ -168,8 +170,12 @@ extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t* in, const uint64_t* off,
     if (n == 0) return hipSuccess;
     // one wave (16 buffers) per workgroup: the waves spread over every CU's load path
     uint32_t threads = n * 4;
-    hipLaunchKernelGGL(lz4mi::lz4mi_xxh32_kernel, dim3((threads + 63) / 64), dim3(64), 0, stream, in, off, len, seed,
-                       hashes, n, standard, dst, dst_off);
+    if (dst)
+        hipLaunchKernelGGL(lz4mi::lz4mi_xxh32_kernel<true>, dim3((threads + 63) / 64), dim3(64), 0, stream, in, off,
+                           len, seed, hashes, n, standard, dst, dst_off);
+    else
+        hipLaunchKernelGGL(lz4mi::lz4mi_xxh32_kernel<false>, dim3((threads + 63) / 64), dim3(64), 0, stream, in, off,
+                           len, seed, hashes, n, standard, dst, dst_off);
     return hipGetLastError();
 }
 
