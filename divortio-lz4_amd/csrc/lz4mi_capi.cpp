@@ -134,18 +134,20 @@ StreamCtx* stream_ctx(hipStream_t s) {
 
 constexpr uint64_t kBitmapChunks0 = 1u << 19;   // initial bitmap capacity: 512 Ki chunks = 64 MiB
 
-// Decoder selection (LZ4MI_DECODER): "auto" (default) = the two-pass ring decoder for
-// blocks compressed at least kRingRatio:1 (long matches: it writes them from LDS), the
-// single-pass kernel for the rest; "ring" = every block through the ring decoder;
-// "single" = the single-pass kernel only.
+// Decoder selection (LZ4MI_DECODER): "single" (default) = the single-pass kernel for
+// every block (with long periodic runs written from LDS it is the faster decoder on
+// every generator measured); "ring" = every block through the
+// two-pass ring decoder; "auto" = the ring decoder for blocks compressed at least
+// kRingRatio:1, the single-pass kernel for the rest (the round-1 dispatch).
 constexpr uint32_t kRingRatio = 32;
 int g_ring_mode = -1;
 uint32_t g_ring_ratio = kRingRatio;
 bool ring_enabled() {
     if (g_ring_mode < 0) {
         const char* e = std::getenv("LZ4MI_DECODER");
-        g_ring_mode = (e && std::strcmp(e, "single") == 0) ? 0 : 1;
-        g_ring_ratio = (e && std::strcmp(e, "ring") == 0) ? 0u : kRingRatio;
+        const bool ring = e && std::strcmp(e, "ring") == 0, autom = e && std::strcmp(e, "auto") == 0;
+        g_ring_mode = (ring || autom) ? 1 : 0;
+        g_ring_ratio = ring ? 0u : kRingRatio;
     }
     return g_ring_mode == 1;
 }
@@ -293,8 +295,14 @@ int32_t lz4mi_debug_ring_stats(uint32_t* out6) {
 }
 
 // Decoder selection for tests / tools: mode 0 single-pass only, 1 ring decoder for blocks
-// compressed at least `ratio`:1 (0: every block). Overrides LZ4MI_DECODER.
+// compressed at least `ratio`:1 (0: every block), -1 back to LZ4MI_DECODER's choice.
+// Overrides LZ4MI_DECODER.
 int32_t lz4mi_debug_set_decoder(int32_t mode, uint32_t ratio) {
+    if (mode < 0) {
+        g_ring_mode = -1;
+        ring_enabled();
+        return LZ4MI_OK;
+    }
     g_ring_mode = mode ? 1 : 0;
     g_ring_ratio = ratio;
     return LZ4MI_OK;

@@ -44,6 +44,9 @@
 #include "lz4mi_common.h"
 #include "lz4mi_decompress.h"
 
+#ifndef LZ4MI_PERIODIC_LDS
+#define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
@@ -87,7 +90,7 @@ constexpr int kB = 4;                         // pieces per lane per pipeline st
 constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 128;               // longer runs are written by the whole wave
-constexpr int kShortPeriodBulk = 1024;        // longer runs of a < 16-byte period use the LDS phase table
+constexpr int kPeriodBulk = 1024;             // longer periodic runs are generated from an LDS copy of the pattern
 constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
 
 struct DecShared {
@@ -108,12 +111,27 @@ struct DecShared {
         uint16_t nxt[kLim];       // parse: next-token table
         uint32_t pme[kLim / 2];   // output: ends of the pending matches
     };
-    union {
-        uint32_t pms[kMaxSeq];    // output: starts of the pending matches
-        uint8_t pat[16 * 16];     // phase table of a long short-period run
-    };
+    uint32_t pms[kMaxSeq];        // output: starts of the pending matches
 };
 static_assert(kLim / 2 >= kMaxSeq, "pending list must fit in the next-token table");
+
+// LDS a whole-wave periodic run may copy its pattern into, by phase of the
+// chunk: round 1 (the pending list is not built yet), rounds 2+ (the staged
+// literals are all written), the cut sequence (all of it; with the F1 check on,
+// all but the sequence tables the check reads afterwards).
+struct PatBuf {
+    uint32_t* w;
+    int32_t bytes;
+};
+__device__ __forceinline__ PatBuf no_pat() { return PatBuf{nullptr, 0}; }   // literal runs
+__device__ __forceinline__ PatBuf pat_round1(DecShared& S) { return PatBuf{S.pms, (int32_t)sizeof(S.pms)}; }
+__device__ __forceinline__ PatBuf pat_rounds(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(S.stage)}; }
+__device__ __forceinline__ PatBuf pat_all(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(DecShared)}; }
+__device__ __forceinline__ PatBuf pat_cut(DecShared& S) {
+    return PatBuf{S.pme, (int32_t)(sizeof(DecShared) - offsetof(DecShared, pme))};
+}
+static_assert(offsetof(DecShared, pms) == offsetof(DecShared, pme) + sizeof(uint32_t) * (kLim / 2),
+              "the cut pattern buffer spans pme and pms");
 
 struct Ctx {
     const uint8_t* blk;   // compressed block
@@ -267,7 +285,10 @@ __device__ __forceinline__ Run match_run(const Ctx& c, int32_t ms, int32_t off, 
     Run M{ms, 0, ms - off, off < ml ? off : 0, R_HIST};
     if (ml == 0 || ms >= c.cap) return M;
     M.n = (ms + ml > c.cap ? c.cap : ms + ml) - ms;
-    if (c.out_off + M.src < 16 || ms + 16 > c.cap) M.kind = R_BYTES;
+    // byte-wise: a dictionary source, a periodic source within 16 bytes of the
+    // buffer start (its two-window pieces would read below it), or an output end
+    // within 16 bytes (a plain source's 16-byte pieces stay inside [src, src + n))
+    if (c.out_off + M.src < 0 || (M.period && c.out_off + M.src < 16) || ms + 16 > c.cap) M.kind = R_BYTES;
     return M;
 }
 // One past the last output byte a match run reads.
@@ -463,7 +484,7 @@ __device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Sl
         if (TWO && mode == 2) v = pick4(A[j], B[j], s[j].k);
         else if (mode == 3) v = expand_period(A[j], s[j].k, s[j].per);
         if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
-            if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pat[0] = 1;
+            if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
         const uint32_t w = s[j].wm & 255u;
@@ -602,7 +623,7 @@ __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSl
     for (int j = 0; j < NB; ++j) {
         if (!s[j].w) continue;
         if (LZ4MI_ABLATE == 4) {
-            if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pat[0] = 1;
+            if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
         out16(c.dst + s[j].y, A[j]);
@@ -653,22 +674,62 @@ __device__ __forceinline__ void lane_slow_run(const Ctx& c, const DecShared& S, 
     }
 }
 
-// Periodic run of period < 16 (long runs of a short pattern): the 16 bytes
-// at each phase are built once in LDS.
-__device__ __forceinline__ void short_period_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+// Long periodic run (match offset < length): the pattern plus 20 bytes of its
+// repetition are copied into LDS, then every 16-byte piece at output distance d
+// is five aligned dword reads at phase d mod period (no history re-reads through
+// the fabric, one output stream per lane). A period longer than the buffer is
+// done in slices of phases, one LDS fill per slice; each slice writes its phase
+// range of every repetition.
+__device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, int lane, const Run& R, PatBuf B) {
     const int32_t per = R.period;
-    __syncthreads();
-    for (int idx = lane; idx < 16 * per; idx += kWave) {
-        const int r = idx >> 4, j = idx & 15;
-        S.pat[idx] = (uint8_t)hist_byte(c, (int64_t)R.src + (r + j) % per);
-    }
-    __syncthreads();
-    const int np = run_pieces(R.n);   // R.n > kShortPeriodBulk: all pieces 16 bytes
-    for (int p = lane; p < np; p += kWave) {
-        const int32_t d = 16 * p < R.n - 16 ? 16 * p : R.n - 16;
-        uint4 v;
-        __builtin_memcpy(&v, S.pat + 16 * (d % per), 16);
-        out16(c.dst + R.y + d, v);
+    const uint8_t* src = c.dst + R.src;
+    const int32_t W = B.bytes - 48;   // phases per slice (the fill covers W + 20 bytes, rounded to 16)
+    const int32_t dl = R.n - 16;      // the last piece (overlaps its predecessor when n % 16)
+    for (int32_t s0 = 0; s0 < per; s0 += W) {
+        const int32_t e0 = per - s0 <= W ? per : s0 + W;   // this slice's phases [s0, e0)
+        __syncthreads();
+        for (int k = lane; 16 * k < e0 - s0 + 20; k += kWave) {
+            const int32_t q = s0 + 16 * k;
+            uint4 v;
+            if (q + 16 <= per) {
+                v = load16<R_HIST>(c, S, R.src + q);
+            } else {
+                unsigned __int128 x = 0;
+#pragma unroll 1
+                for (int j = 0; j < 16; ++j) x |= (unsigned __int128)src[(q + j) % per] << (8 * j);
+                __builtin_memcpy(&v, &x, 16);
+            }
+            B.w[4 * k] = v.x;
+            B.w[4 * k + 1] = v.y;
+            B.w[4 * k + 2] = v.z;
+            B.w[4 * k + 3] = v.w;
+        }
+        __syncthreads();
+        if (e0 - s0 == per) {   // one slice: every piece, the phase carried from piece to piece
+            const int32_t np = run_pieces(R.n);
+            const int32_t step = (16 * kWave) % per;
+            int32_t r = (16 * lane) % per;
+#pragma unroll 1
+            for (int32_t p = lane; p < np; p += kWave) {
+                const bool last = 16 * p > dl;
+                const int32_t d = last ? dl : 16 * p;
+                const uint4 v = stage16(B.w, last ? d % per : r);
+                if (LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, v);
+                r += step;
+                if (r >= per) r -= per;
+            }
+        } else {                // pieces at 16-aligned d with phase in [s0, e0), repetition by repetition
+#pragma unroll 1
+            for (int32_t base = 0; base + s0 <= dl; base += per) {
+                const int32_t lo = base + s0, hi = base + e0 < dl + 1 ? base + e0 : dl + 1;
+#pragma unroll 1
+                for (int32_t d = ((lo + 15) & ~15) + 16 * lane; d < hi; d += 16 * kWave)
+                    if (LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, d - base - s0));
+            }
+            const int32_t ph = dl % per;
+            if ((R.n & 15) && lane == 0 && ph >= s0 && ph < e0 && LZ4MI_ABLATE != 4)
+                out16(c.dst + R.y + dl, stage16(B.w, ph - s0));
+        }
     }
     __syncthreads();
 }
@@ -694,10 +755,14 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
 }
 
 // The whole wave writes one run (uniform R).
-__device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R) {
+__device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R, PatBuf B) {
     if (R.kind == R_NONE || R.n <= 0) return;
-    if (R.kind == R_HIST && R.period && R.period < 16 && R.n > kShortPeriodBulk) {
-        short_period_run(c, S, lane, R);
+    // (a byte-wise periodic run whose source is inside the buffer qualifies too:
+    // periodic_run reads only [src, src + period))
+    const bool in_buf = R.kind == R_HIST || (R.kind == R_BYTES && c.out_off + R.src >= 0);
+    if (LZ4MI_PERIODIC_LDS && in_buf && R.period && R.n > kPeriodBulk &&
+        B.bytes > 0 && (R.period + 48 <= B.bytes || (R.n >= 4 * R.period && B.bytes >= 1024))) {
+        periodic_run(c, S, lane, R, B);
         return;
     }
     const int np = run_pieces(R.n);
@@ -1227,10 +1292,10 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             lane_literals(c, S, longL ? no_run() : L);
             lane_literals(c, S, longML ? no_run() : ML);
             PROF(17);
-            for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)));
+            for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)), no_pat());
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
-            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)));
-            for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
+            for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_round1(S));
             PROF(18);
         }
         {
@@ -1282,7 +1347,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
                 if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
                 if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
-                for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)));
+                for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_rounds(S));
             }
             {
                 LaneMatchGen g{c, S, ready, 0u, lane, 0, 0, 0, 0, 0};
@@ -1295,11 +1360,11 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             PROF_COUNT(12, 1);
             const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
             if (e) { status = err_status(e); break; }
-            wave_run(c, S, lane, Run{(int32_t)tab_hi, (int32_t)cll, (int32_t)clit, 0, cll ? (uint32_t)R_COMP : (uint32_t)R_NONE});
+            wave_run(c, S, lane, Run{(int32_t)tab_hi, (int32_t)cll, (int32_t)clit, 0, cll ? (uint32_t)R_COMP : (uint32_t)R_NONE}, no_pat());
             const Run M = match_run(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
             if (M.n > 0) {
                 wait_vmem();    // everything below the match is read back as history
-                wave_run(c, S, lane, M);
+                wave_run(c, S, lane, M, a.f1check ? pat_cut(S) : pat_all(S));
             }
         }
 #else

@@ -19,12 +19,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _ring_for_every_block():
-    """Route every block through the ring decoder (the default routes only >= 32:1 blocks)."""
+    """Route every block through the ring decoder (the default is the single-pass kernel)."""
     import lz4mi
     lz4mi.init(0)
     lz4mi.lib().lz4mi_debug_set_decoder(1, 0)
     yield
-    lz4mi.lib().lz4mi_debug_set_decoder(1, 32)
+    lz4mi.lib().lz4mi_debug_set_decoder(-1, 0)
 
 
 def _lz4mi():

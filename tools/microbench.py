@@ -20,6 +20,51 @@ sys.path.insert(0, os.path.join(ROOT, "divortio-lz4_amd"))
 BLOCK = 4 << 20
 
 
+def make_raw(torch, lz4mi, gen, n, sp):
+    """n x 4 MiB raw blocks on the device: device generators (tiles216, random,
+    repetitive), bench.py's "mix", or host-made blocks (copy, runs, text from the
+    oracle's generators; per:<P> = P random bytes repeated; far = copies of 8-48 KiB
+    windows from the previous 64 KiB, non-overlapping), 16 distinct blocks tiled."""
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    if gen == "mix":   # bench.py's 50/50 random/tiles216 mix (same shuffle)
+        sys.path.insert(0, ROOT)
+        from bench import mix_order
+        tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+        for b, kind in enumerate(mix_order(n)):
+            lz4mi.generate_blocks_dev(tmp.data_ptr(), kind, 1 + b, BLOCK, 1, sp)
+            raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+    elif gen in lz4mi.GENERATORS:
+        lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+    else:   # host-made: oracle generators (copy, runs, text) or per:<P> (P random bytes
+        #     repeated), 16 distinct blocks tiled over the batch
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        rng = np.random.default_rng(5)
+        host = []
+        for k in range(16):
+            if gen == "far":
+                b = np.empty(BLOCK, dtype=np.uint8)
+                b[:65536] = rng.integers(0, 256, 65536, dtype=np.uint8)
+                pos = 65536
+                while pos < BLOCK:
+                    ln = min(int(rng.integers(8192, 49152)), BLOCK - pos)
+                    src = pos - int(rng.integers(ln, 65536))
+                    b[pos:pos + ln] = b[src:src + ln]
+                    pos += ln
+                host.append(b)
+            elif gen.startswith("per:"):
+                P = int(gen[4:])
+                host.append(np.resize(rng.integers(0, 256, P, dtype=np.uint8), BLOCK))
+            else:
+                host.append(O.generate(gen, 1 + k, BLOCK))
+        hb = torch.from_numpy(np.concatenate(host)).cuda()
+        for b in range(0, n, 16):
+            m = min(16, n - b)
+            raw[b * BLOCK:(b + m) * BLOCK].copy_(hb[:m * BLOCK])
+    return raw
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gens", default="tiles216,random,repetitive")
@@ -48,16 +93,7 @@ def main():
     n = args.blocks
     res = {}
     for gen in args.gens.split(","):
-        raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-        if gen == "mix":   # bench.py's 50/50 random/tiles216 mix (same shuffle)
-            sys.path.insert(0, ROOT)
-            from bench import mix_order
-            tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
-            for b, kind in enumerate(mix_order(n)):
-                lz4mi.generate_blocks_dev(tmp.data_ptr(), kind, 1 + b, BLOCK, 1, sp)
-                raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
-        else:
-            lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+        raw = make_raw(torch, lz4mi, gen, n, sp)
         slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
         comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
         roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK

@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--blocks", default="256,1024,4096")
     a = ap.parse_args()
     import torch, lz4mi
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from microbench import make_raw
     lz4mi.init(0)
     L = ctypes.CDLL(a.so)
     L.lz4mi_decompress_blocks.argtypes = lz4mi.lib().lz4mi_decompress_blocks.argtypes
@@ -24,8 +26,7 @@ def main():
     buf = (ctypes.c_ulonglong * 24)()
     for gen in a.gens.split(","):
         for n in map(int, a.blocks.split(",")):
-            raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-            lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+            raw = make_raw(torch, lz4mi, gen, n, sp)
             slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
             comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
             roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
