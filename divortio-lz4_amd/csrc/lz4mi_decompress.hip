@@ -678,8 +678,8 @@ __device__ __forceinline__ void lane_slow_run(const Ctx& c, const DecShared& S, 
 // repetition are copied into LDS, then every 16-byte piece at output distance d
 // is five aligned dword reads at phase d mod period (no history re-reads through
 // the fabric, one output stream per lane). A period longer than the buffer is
-// done in slices of phases, one LDS fill per slice; each slice writes its phase
-// range of every repetition.
+// done in slices of phases, one LDS fill and one pass over the run per slice,
+// each pass writing the pieces whose phase falls in its slice.
 __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, int lane, const Run& R, PatBuf B) {
     const int32_t per = R.period;
     const uint8_t* src = c.dst + R.src;
@@ -705,30 +705,18 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
             B.w[4 * k + 3] = v.w;
         }
         __syncthreads();
-        if (e0 - s0 == per) {   // one slice: every piece, the phase carried from piece to piece
-            const int32_t np = run_pieces(R.n);
-            const int32_t step = (16 * kWave) % per;
-            int32_t r = (16 * lane) % per;
+        // every piece whose phase falls in this slice; the phase is carried from piece to piece
+        const int32_t np = run_pieces(R.n);
+        const int32_t step = (16 * kWave) % per;
+        int32_t r = (16 * lane) % per;
 #pragma unroll 1
-            for (int32_t p = lane; p < np; p += kWave) {
-                const bool last = 16 * p > dl;
-                const int32_t d = last ? dl : 16 * p;
-                const uint4 v = stage16(B.w, last ? d % per : r);
-                if (LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, v);
-                r += step;
-                if (r >= per) r -= per;
-            }
-        } else {                // pieces at 16-aligned d with phase in [s0, e0), repetition by repetition
-#pragma unroll 1
-            for (int32_t base = 0; base + s0 <= dl; base += per) {
-                const int32_t lo = base + s0, hi = base + e0 < dl + 1 ? base + e0 : dl + 1;
-#pragma unroll 1
-                for (int32_t d = ((lo + 15) & ~15) + 16 * lane; d < hi; d += 16 * kWave)
-                    if (LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, d - base - s0));
-            }
-            const int32_t ph = dl % per;
-            if ((R.n & 15) && lane == 0 && ph >= s0 && ph < e0 && LZ4MI_ABLATE != 4)
-                out16(c.dst + R.y + dl, stage16(B.w, ph - s0));
+        for (int32_t p = lane; p < np; p += kWave) {
+            const bool last = 16 * p > dl;
+            const int32_t d = last ? dl : 16 * p;
+            const int32_t ph = (last ? d % per : r) - s0;
+            if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, ph));
+            r += step;
+            if (r >= per) r -= per;
         }
     }
     __syncthreads();

@@ -52,7 +52,8 @@ def tables(seqs):
 
 def model(comp):
     seqs = parse(comp)
-    st = dict(tables=0, matches=0, pend=0, pend_per=0, segs=0, hops=0, maxhops=0, rounds=0)
+    st = dict(tables=0, matches=0, pend=0, pend_per=0, segs=0, hops=0, maxhops=0, rounds=0, gsegs=0, grp_g=0, grp_s=0,
+              fail8=0)
     for T in tables(seqs):
         st["tables"] += 1
         O_ = T[0][1]
@@ -83,18 +84,30 @@ def model(comp):
             if not ok:
                 pend.append(k); st["pend"] += 1; st["pend_per"] += per
         # segment chase for the pending ones
+        lane_g = {}; lane_s = {}
         for k in pend:
             _, y, ll, lit, off, ml = T[k]
+            if off < ml: continue
             pos, end = y + ll, y + ll + ml
+            failed = False
             while pos < end:
-                a = pos - off; n = end - pos; h = 0
+                a = pos - off; n = min(end - pos, 16); h = 0
                 while a >= O_:
                     kind, kk, pe = piece(a)
                     n = min(n, pe - a)
                     if kind == 0: break
                     a -= T[kk][4]; h += 1
+                if a < O_:
+                    n = min(n, O_ - a); st["gsegs"] += 1
+                    lane_g[k] = lane_g.get(k, 0) + 1
+                lane_s[k] = lane_s.get(k, 0) + 1
+                if h > 8: failed = True
                 st["segs"] += 1; st["hops"] += h; st["maxhops"] = max(st["maxhops"], h)
                 pos += n
+            st["fail8"] += failed
+        for g in range(0, len(T), 64):
+            st["grp_g"] += max([lane_g.get(k, 0) for k in range(g, g + 64)] + [0])
+            st["grp_s"] += max([lane_s.get(k, 0) for k in range(g, g + 64)] + [0])
         # rounds under the current rule (pending match ready when its source meets no pending match)
         done = set(range(len(T))) - set(pend)
         r = 0
@@ -123,4 +136,6 @@ if __name__ == "__main__":
         print(gen, "ratio %.2f" % (len(src) / len(comp)), "tables", t,
               "matches/table %.1f" % (s["matches"] / t), "pending/table %.2f (periodic %.2f)" % (s["pend"] / t, s["pend_per"] / t),
               "segments/pending %.2f" % (s["segs"] / max(1, s["pend"])), "hops/segment %.2f max %d" % (s["hops"] / max(1, s["segs"]), s["maxhops"]),
-              "rounds/table %.2f" % (s["rounds"] / t), flush=True)
+              "rounds/table %.2f" % (s["rounds"] / t),
+              "global segs/pending %.2f" % (s["gsegs"] / max(1, s["pend"])),
+              "per table: sum over groups of max-lane segs %.2f, global segs %.2f; >8 hops %.2f" % (s["grp_s"] / t, s["grp_g"] / t, s["fail8"] / t), flush=True)
