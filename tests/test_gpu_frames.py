@@ -226,7 +226,11 @@ def test_ring_decoder_bitmap_overflow_falls_back_exactly(monkeypatch):
     lz4mi.generate_blocks_dev(raw.data_ptr(), "repetitive", 3, bs, n, _stream())
     srcs = [raw[b * bs:(b + 1) * bs].cpu().numpy() for b in range(n)]
     comps = [O.compress_block_bytes(x) for x in srcs]
-    st, outs, _ = lz4mi.decompress_blocks(comps, [bs] * n)
+    lz4mi.lib().lz4mi_debug_set_decoder(1, 32)   # the round-1 dispatch: ring decoder for >= 32:1 blocks
+    try:
+        st, outs, _ = lz4mi.decompress_blocks(comps, [bs] * n)
+    finally:
+        lz4mi.lib().lz4mi_debug_set_decoder(-1, 0)
     assert (st == 0).all()
     for s, o in zip(srcs, outs):
         assert np.array_equal(s, o)
