@@ -250,10 +250,16 @@ __device__ __forceinline__ SeqInfo seq_info(const DecShared& S, uint32_t k) {
     return SeqInfo{(int32_t)(v.x & 0xFFFF), (int32_t)(v.x >> 16), (int32_t)(v.y & 0xFFFF), (int32_t)(v.y >> 16)};
 }
 
+// History (earlier output of this wave) is read with plain loads: the CU's L1 sees
+// the wave's own completed stores (every read of output follows an s_waitcnt on
+// the stores that wrote it), and L2 keeps the lines. Nontemporal loads (used
+// until round 2) cost tiles216 17 % (19.15 vs 15.87 ms, one process, same box).
+__device__ __forceinline__ uint32_t hist_u8(const uint8_t* p) { return *p; }
+
 // Byte of earlier output at block-relative position pos (dictionary below out[0]).
 __device__ __forceinline__ uint32_t hist_byte(const Ctx& c, int64_t pos) {
     int64_t abs = c.out_off + pos;
-    if (abs >= 0) return ld_nt_u8(c.dst + pos);
+    if (abs >= 0) return hist_u8(c.dst + pos);
     return c.dict ? c.dict[c.dict_len + abs] : 0u;
 }
 
@@ -349,40 +355,6 @@ __device__ __forceinline__ Piece plan_piece(const Run& R, int p) {
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// w bytes from an unaligned address (gfx950 runs in unaligned-access mode);
-// NT: bypass L1 (bytes this wave stored earlier in the launch).
-template <bool NT>
-__device__ __forceinline__ uint4 load_w(const uint8_t* p, uint32_t w) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (w == 16) {
-        if (NT) {
-            u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)p);
-            v = make_uint4(t.x, t.y, t.z, t.w);
-        } else {
-            __builtin_memcpy(&v, p, 16);
-        }
-    } else if (w == 8) {
-        if (NT) {
-            u32x2_t t = __builtin_nontemporal_load((const u32x2_t*)p);
-            v.x = t.x;
-            v.y = t.y;
-        } else {
-            __builtin_memcpy(&v, p, 8);
-        }
-    } else if (w == 4) {
-        if (NT) v.x = __builtin_nontemporal_load((const uint32_t*)p);
-        else __builtin_memcpy(&v.x, p, 4);
-    } else if (w == 2) {
-        uint16_t t;
-        if (NT) t = __builtin_nontemporal_load((const uint16_t*)p);
-        else __builtin_memcpy(&t, p, 2);
-        v.x = t;
-    } else {
-        v.x = NT ? (uint32_t)__builtin_nontemporal_load(p) : (uint32_t)*p;
-    }
-    return v;
-}
-
 __device__ __forceinline__ void store_w(uint8_t* p, uint4 v, uint32_t w) {
     if (w == 16) {
         __builtin_memcpy(p, &v, 16);
@@ -456,7 +428,7 @@ __device__ __forceinline__ uint4 load16(const Ctx& c, const DecShared& S, int32_
     } else if (KIND == R_COMP) {
         __builtin_memcpy(&v, c.blk + a, 16);
     } else {
-        const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(c.dst + a));
+        const u32x4_t t = *(const u32x4_t*)(c.dst + a);
         v = make_uint4(t.x, t.y, t.z, t.w);
     }
     return v;
@@ -611,7 +583,7 @@ __device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], ui
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         if (s[j].w) {
-            const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(c.dst + s[j].a));
+            const u32x4_t t = *(const u32x4_t*)(c.dst + s[j].a);
             A[j] = make_uint4(t.x, t.y, t.z, t.w);
         }
     }
@@ -855,7 +827,7 @@ __device__ __forceinline__ uint32_t f1_changes(const Ctx& c, int32_t ms, int32_t
     const int32_t p0 = ms + ml - 8;
     if (p0 - off < 0) return c.isolate ? 2u : 1u;
     for (int32_t p = p0; p < ms && p < c.cap; ++p)
-        if (ld_nt_u8(c.dst + p) != ld_nt_u8(c.dst + p - off)) return 1;
+        if (hist_u8(c.dst + p) != hist_u8(c.dst + p - off)) return 1;
     return 0;
 }
 
@@ -891,7 +863,7 @@ __device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t ns
                 for (int32_t t = lane; t < ml; t += kWave) {
                     const int64_t d = ms + t;
                     const int64_t s = ms - off + (off < ml ? t % off : t);
-                    const uint32_t v = ld_nt_u8(c.dst + s);
+                    const uint32_t v = hist_u8(c.dst + s);
                     if (d < c.cap) c.dst[d] = (uint8_t)v;
                 }
             } else if (lane == 0) {   // spills from the dictionary into the output: in order, byte by byte
@@ -905,7 +877,7 @@ __device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t ns
         if (internal && off >= 8 && ml < 8) {
             const int64_t p = ms + ml - 8 + lane;
             const bool mine = lane < 8 - ml && c.out_off + p >= 0 && p < c.cap;
-            const uint32_t v = mine ? (c.out_off + p - off >= 0 ? ld_nt_u8(c.dst + p - off) : 0u) : 0u;
+            const uint32_t v = mine ? (c.out_off + p - off >= 0 ? hist_u8(c.dst + p - off) : 0u) : 0u;
             if (mine) c.dst[p] = (uint8_t)v;
             const int64_t p0 = ms + ml - 8;
             if (p0 < lo) lo = p0;
