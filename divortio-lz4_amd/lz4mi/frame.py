@@ -156,7 +156,8 @@ def _content_checksum(raw, group, root, rank, world, sizes, dist):
             else:
                 b = bufs[k % 2][:m]
                 dist.recv(b, src=r, group=group)
-                host = b.cpu().numpy()
+                # a copy even for a CPU buffer: b is reused while the worker may still hash this piece
+                host = b.to("cpu", copy=True).numpy()
             k += 1
             w.feed(host)
     return w.digest()
