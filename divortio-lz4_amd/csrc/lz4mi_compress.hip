@@ -631,11 +631,12 @@ __global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
 // Batch encoder with the hash tables in global memory: one Int32Array(16384)
 // per block (values = position + 1, as the reference's), so LDS only holds the
 // output ring and 16 blocks run per CU instead of 4. A probe at the chain's
-// head reads and replaces its table slot with one atomic exchange (the
-// reference's insert-before-verify in a single operation); after a miss the
-// following probes go as a 64-wide batch like compress_block_fast's (table read
-// with plain L1-bypassing loads, the probes that happen store their positions,
-// and the stores complete before the next table access).
+// head reads and replaces its table slot (the reference's insert-before-verify);
+// after a miss the following probes go as a 64-wide batch like
+// compress_block_fast's (the probes that happen store their positions, and the
+// stores complete before the next table access). Table reads are plain loads:
+// the CU's L1 sees the wave's own completed stores (nontemporal loads and an
+// atomic exchange at the head, used until round 2, cost 7 %: 208.8 vs 194.5 ms).
 struct GtShared {
     uint8_t ring[kRing];
     uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
@@ -667,7 +668,10 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         }
         const uint32_t h0 = (seq0 * kP1) >> 18;
         int32_t old = 0;
-        if (lane == 0) old = atomicExch(&T[h0], i + 1);
+        if (lane == 0) {   // read and replace (one wave owns the table: no atomic needed)
+            old = T[h0];
+            T[h0] = i + 1;
+        }
         old = (int32_t)uniform((uint32_t)old);
         int32_t cand0 = old - 1;
         if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
@@ -749,7 +753,7 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         const int nb = __popcll(__ballot(act));
         int32_t cand = -1;
         if (act) {
-            const int32_t ov = __builtin_nontemporal_load(&T[h]);
+            const int32_t ov = T[h];
             cand = ov - 1;
             if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
         }
