@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--so", nargs="*", default=[])
     ap.add_argument("--what", default="decompress")
     ap.add_argument("--skip-default", action="store_true", help="time only the --so libraries")
+    ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="extra decode flags (0x8 = LZ4MI_JS_EXACT)")
     args = ap.parse_args()
     import torch
     import lz4mi
@@ -112,7 +113,7 @@ def main():
                 if args.what == "decompress":
                     r = L.lz4mi_decompress_blocks(comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), dec.data_ptr(),
                                                   roff.data_ptr(), rlen.data_ptr(), None, 0, dlen.data_ptr(),
-                                                  st.data_ptr(), n, 1, sp)
+                                                  st.data_ptr(), n, 1 | args.flags, sp)
                 else:
                     r = L.lz4mi_compress_blocks(raw.data_ptr(), roff.data_ptr(), rlen.data_ptr(), comp.data_ptr(),
                                                 coff.data_ptr(), clen.data_ptr(), n, 1, sp)
