@@ -448,11 +448,11 @@ __device__ void ring_reload(RingShared& S, const uint8_t* dst, int32_t lo, int32
     for (int32_t u = u0 + 16 * tid; u < hi; u += 16 * kThreads) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (u + 16 <= cap) {
-            const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(dst + u));
+            const u32x4_t t = *(const u32x4_t*)(dst + u);
             v = make_uint4(t.x, t.y, t.z, t.w);
         } else {
             unsigned __int128 x = 0;
-            for (int j = 0; j < 16 && u + j < cap; ++j) x |= (unsigned __int128)ld_nt_u8(dst + u + j) << (8 * j);
+            for (int j = 0; j < 16 && u + j < cap; ++j) x |= (unsigned __int128)*(dst + u + j) << (8 * j);
             __builtin_memcpy(&v, &x, 16);
         }
         __builtin_memcpy(S.ring + (u & kRingMask), &v, 16);
@@ -542,7 +542,7 @@ __device__ void direct_match(uint8_t* pat, uint8_t* dst, int32_t ms, int32_t off
         __syncthreads();
         for (int idx = tid; idx < 16 * per; idx += kThreads) {
             const int r = idx >> 4, j = idx & 15;
-            pat[idx] = ld_nt_u8(dst + src + (r + j) % per);
+            pat[idx] = *(dst + src + (r + j) % per);
         }
         __syncthreads();
     }
@@ -558,16 +558,16 @@ __device__ void direct_match(uint8_t* pat, uint8_t* dst, int32_t ms, int32_t off
             piece_at(n, p < np ? p : np - 1, dd[j], ww[j]);
             const int32_t d = dd[j];
             if (per == 0) {
-                const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(dst + src + d));
+                const u32x4_t t = *(const u32x4_t*)(dst + src + d);
                 v[j] = make_uint4(t.x, t.y, t.z, t.w);
             } else if (per < 16) {
                 __builtin_memcpy(&v[j], pat + 16 * (d % per), 16);
             } else {
                 const int32_t r = d % per;
-                const u32x4_t t = __builtin_nontemporal_load((const u32x4_t*)(dst + src + r));
+                const u32x4_t t = *(const u32x4_t*)(dst + src + r);
                 v[j] = make_uint4(t.x, t.y, t.z, t.w);
                 if (r + 16 > per) {   // the window wraps: bytes [per - r, 16) restart at the period's start
-                    const u32x4_t t2 = __builtin_nontemporal_load((const u32x4_t*)(dst + src));
+                    const u32x4_t t2 = *(const u32x4_t*)(dst + src);
                     v[j] = splice(v[j], make_uint4(t2.x, t2.y, t2.z, t2.w), per - r);
                 }
             }
@@ -668,7 +668,7 @@ __device__ __noinline__ uint4 make_unit(const RingShared& S, const Step& st, int
             uint4 v = make_uint4(0, 0, 0, 0);
             unsigned __int128 x = 0;
             for (int j = 0; j < 16; ++j)
-                if (p + j >= 0) x |= (unsigned __int128)ld_nt_u8(dst + p + j) << (8 * j);
+                if (p + j >= 0) x |= (unsigned __int128)*(dst + p + j) << (8 * j);
             __builtin_memcpy(&v, &x, 16);
             return v;
         }
