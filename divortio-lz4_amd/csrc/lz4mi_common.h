@@ -69,10 +69,9 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
 // (stores acknowledged by L2). Also a compiler memory barrier.
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Global loads that bypass the CU's L1 (served from L2): used for every read of
-// bytes this wave itself wrote earlier, so a line cached before the write can
-// never be observed stale.
-__device__ __forceinline__ uint32_t ld_nt_u32(const uint32_t* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ uint8_t ld_nt_u8(const uint8_t* p) { return __builtin_nontemporal_load(p); }
+// Reads of bytes this wave (or workgroup) wrote earlier in the launch are plain
+// loads: the CU's L1 is coherent with the CU's own completed stores (the LLVM
+// AMDGPU memory model needs no L1 invalidate for workgroup scope on gfx950), and
+// every such read follows an s_waitcnt on the stores that wrote the bytes.
 
 }  // namespace lz4mi
