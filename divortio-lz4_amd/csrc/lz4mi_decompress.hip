@@ -886,10 +886,6 @@ __device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t ns
     }
 }
 
-// BM: the chunk's token starts come from pass 1's bitmap (lz4mi_decompress_ring.hip)
-// instead of the next-token table / jump tables / speculative walks; chunks are then
-// the fixed 1 KiB chunks of the bitmap, staged from their base.
-template <bool BM>
 __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     __shared__ DecShared S;
     const int lane = threadIdx.x;
@@ -912,8 +908,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
     bool have_pf = false;
     int64_t pf_at = -1;                    // compressed position pf0/pf1 were loaded from
-    uint32_t pfm = 0;                      // (BM) the bitmap bits of the prefetched chunk, this lane's segment
-    const uint16_t* bm16 = BM ? (const uint16_t*)(a.bitmap + (uint64_t)a.chunk_base[b] * (kChunk / 64)) : nullptr;
 #if LZ4MI_PROFILE
     uint64_t prof[24] = {0};
     uint64_t prof_t = wall_clock64();
@@ -921,14 +915,11 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
     while (c.ip < c.in_len) {
         PROF_COUNT(10, 1);
-        const int32_t entry = c.ip;               // the true next token
-        if (BM) c.ip = entry & ~(kChunk - 1);     // stage from the chunk's base
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
         // the previous chunk's output phase, ahead of its stores) -------------
         if (!have_pf || pf_at != c.ip) {
             pf0 = stage_piece(c, (int64_t)c.ip + 16 * lane);
             if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, (int64_t)c.ip + 16 * (kWave + lane));
-            if (BM) pfm = bm16[(c.ip / kChunk) * 64 + lane];
             settle(pf0);
             settle(pf1);
         }
@@ -941,44 +932,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
         const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
         uint32_t vis, tail;
-        if (BM) {
-            PROF(0);
-            // ---- 2-3. the chunk's tokens from pass 1's bitmap, from the true entry on
-            const uint32_t rel = (uint32_t)(entry - c.ip);
-            vis = pfm & 0xFFFFu;
-            if (seg0 + 16 <= rel) vis = 0;
-            else if (seg0 < rel) vis &= ~((1u << (rel - seg0)) - 1u);
-            if (!__ballot(lane == (int)(rel >> 4) && ((vis >> (rel & 15)) & 1u))) {
-                // pass 1's walk was off the true chain at the entry: walk the true chain
-                // until it lands on a token of pass 1's walk (from there on they coincide)
-                S.nxt[lane] = (uint16_t)vis;
-                S.nxt[64 + lane] = 0;
-                __syncthreads();
-                if (lane == 0) {
-                    uint32_t p = rel;
-                    while (p < (uint32_t)kChunk && p < rem) {
-                        if ((S.nxt[p >> 4] >> (p & 15)) & 1u) break;
-                        S.nxt[64 + (p >> 4)] |= (uint16_t)(1u << (p & 15));
-                        const uint32_t q = next_token(s, p, rem);
-                        if (q >= kEnd) {   // the last token of the chunk: nothing of pass 1's after it
-                            p = kChunk;
-                            break;
-                        }
-                        p = q;
-                    }
-                    S.nxt[128] = (uint16_t)(p < (uint32_t)kChunk ? p : (uint32_t)kChunk);
-                }
-                __syncthreads();
-                const uint32_t ps = S.nxt[128];
-                if (seg0 + 16 <= ps) vis = 0;
-                else if (seg0 < ps) vis &= ~((1u << (ps - seg0)) - 1u);
-                vis |= S.nxt[64 + lane];
-                __syncthreads();
-            }
-            const uint64_t hv = __ballot(vis != 0);
-            const uint32_t lt = lane_val(seg0 + 31 - __builtin_clz(vis | 1u), (uint32_t)(63 - __builtin_clzll(hv)));
-            tail = uniform(next_token(s, lt, rem));   // where the chain leaves the chunk
-        } else {
+        {
         PROF(0);
         // ---- 2. next-token table -----------------------------------------
         uint16_t* nxt = S.nxt;
@@ -1067,10 +1021,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (!cut && tail < kEnd && (int64_t)c.ip + tail < c.in_len) {
             // the next chunk's bytes: loaded while this chunk's table is built
             int64_t nip = (int64_t)c.ip + tail;
-            if (BM) nip &= ~(int64_t)(kChunk - 1);
             pf0 = stage_piece(c, nip + 16 * lane);
             if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
-            if (BM) pfm = bm16[(nip / kChunk) * 64 + lane];
             pf_at = nip;
             have_pf = true;
         }
@@ -1186,11 +1138,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (cut) {   // the next chunk's bytes: their loads go out before this chunk's stores
             int64_t nip = cq < c.in_len ? cq : c.in_len;
             if (nip < c.in_len) {
-                if (BM) nip &= ~(int64_t)(kChunk - 1);
-                pf0 = stage_piece(c, nip + 16 * lane);
+                    pf0 = stage_piece(c, nip + 16 * lane);
                 if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
-                if (BM) pfm = bm16[(nip / kChunk) * 64 + lane];
-                pf_at = nip;
+                    pf_at = nip;
                 have_pf = true;
             }
         }
@@ -1367,7 +1317,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     }
 }
 
-__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block<false>(a); }
+__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block(a); }
 
 }  // namespace lz4mi
 
