@@ -275,6 +275,32 @@ def napi_e2e(batch, nblocks=64):
             os.remove(path)
 
 
+def reference_benchmark(with_js):
+    """The reference's own published benchmark shape (docs/BENCHMARKS.md: LZ4.compress /
+    decompress of 25 MB of repeated JSON, 4 MiB independent blocks) through the drop-in
+    (tools/json_workload.mjs, host buffers, PCIe-inclusive), the pure-JS block codec on one
+    core of this box on the same data (cpu_baseline leg), and the published numbers."""
+    r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "tools", "json_workload.mjs"), "25", "5"],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    out = {"workload": "LZ4.compress(x, null, 4194304, true, false) / LZ4.decompress of 25 MiB of one JSON record "
+                       "repeated (the shape of the reference's benchmark data), host buffers through N-API; MB = 2^20 B",
+           "drop_in": json.loads(r.stdout.strip().splitlines()[-1]),
+           "published_reference_MBps": {"compress_25MB": 484, "decompress_25MB": 459,
+                                        "hardware": "MacBook Pro mid-2015 (i7 quad, Node 24), docs/BENCHMARKS.md"}}
+    if with_js:
+        j = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "oracle", "js_cpu_baseline.mjs"), "json", "1", "6"],
+                           capture_output=True, text=True, timeout=600)
+        if j.returncode == 0:
+            d = json.loads(j.stdout.strip().splitlines()[-1])
+            out["pure_js_1core_MBps"] = {"compress": round(d["compress_GBps"] * 1e9 / (1 << 20), 1),
+                                         "decompress": round(d["decompress_GBps"] * 1e9 / (1 << 20), 1),
+                                         "sample": "oracle/lz4_js.mjs block codec, 6 x 4 MiB blocks, 1 worker_thread, "
+                                                   f"{d['cpu_model']}, node {d['node']}"}
+    return out
+
+
 def pmc_traffic(lz4mi, n, gen):
     """HBM bytes per decode launch from the committed rocprofv3 PMC passes, used only when
     they were measured on this exact build and workload (else null)."""
@@ -401,6 +427,7 @@ def main():
         line["variants"] = extra
     if napi is not None:
         line["napi_end_to_end"] = napi
+        line["reference_benchmark"] = reference_benchmark(bool(args.cpu_baseline))
     if args.cpu_baseline and rank == 0 and world == 1:
         line["cpu_baseline"] = js_cpu_baseline(args.gen if args.gen in ("tiles216", "random", "repetitive")
                                                else "tiles216", args.cpu_blocks)

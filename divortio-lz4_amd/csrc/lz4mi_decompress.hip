@@ -1271,11 +1271,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
             if (e) { status = err_status(e); break; }
             wave_run(c, S, lane, Run{(int32_t)tab_hi, (int32_t)cll, (int32_t)clit, 0, cll ? (uint32_t)R_COMP : (uint32_t)R_NONE}, no_pat());
-            const Run M = match_run(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
-            if (M.n > 0) {
-                wait_vmem();    // everything below the match is read back as history
-                wave_run(c, S, lane, M, a.f1check ? pat_cut(S) : pat_all(S));
-            }
         }
 #else
         if (cut) {
@@ -1291,10 +1286,27 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 const SeqInfo q = seq_info(S, k);
                 dv |= f1_changes(c, (int32_t)S.t_out[k] + q.ll, q.off, q.ml);
             }
-            if (cut && lane == 0) dv |= f1_changes(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
             if (__ballot(dv & 2u)) { status = -9; break; }
-            if (__ballot(dv)) f1_fixup(c, S, lane, nseq, cut, (int64_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
+            if (__ballot(dv)) f1_fixup(c, S, lane, nseq, false, 0, 0, 0);
         }
+#if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
+        // the cut sequence's match, after the table's F1 replay (it reads the replayed
+        // bytes, as the reference's copy does); the tables are idle now: all of LDS
+        // can hold a periodic pattern
+        if (cut) {
+            const Run M = match_run(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
+            if (M.n > 0) {
+                wait_vmem();    // everything below the match is read back as history
+                wave_run(c, S, lane, M, pat_all(S));
+            }
+            if (a.f1check) {    // its own tail rewrite, after its copy as in the reference
+                wait_vmem();
+                const uint32_t dv = lane == 0 ? f1_changes(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml) : 0u;
+                if (__ballot(dv & 2u)) { status = -9; break; }
+                if (__ballot(dv)) f1_fixup(c, S, lane, 0, true, (int64_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml);
+            }
+        }
+#endif
         c.O = tab_hi;
         if (cut) {
             c.O += cll + cml;

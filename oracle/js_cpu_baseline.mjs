@@ -13,7 +13,11 @@
 import os from 'os';
 import fs from 'fs';
 import { Worker, isMainThread, parentPort, workerData } from 'worker_threads';
-import { compressBlock, decompressBlock, generate } from './lz4_js.mjs';
+import { compressBlock, decompressBlock, generate as generateBlock } from './lz4_js.mjs';
+import { jsonRepeat } from '../tools/json_data.mjs';
+
+// 'json': the reference's benchmark data shape (tools/json_data.mjs), same bytes in every block
+const generate = (gen, seed, n) => (gen === 'json' ? jsonRepeat(n) : generateBlock(gen, seed, n));
 
 const BLOCK = 4 << 20;
 

@@ -134,3 +134,40 @@ def test_periodic_runs_single_pass(source):
             assert k == 0 and np.array_equal(o, e), i
     finally:
         lz4mi.lib().lz4mi_debug_set_decoder(-1, 0)
+
+
+def json_blocks():
+    """The reference benchmark's data shape (tools/json_data.mjs: one JSON record repeated):
+    short F1-eligible matches inside the first record, then one periodic match running to
+    the block end as the chunk's cut sequence — the F1 replay and the long match in one chunk."""
+    import json
+    rec = json.dumps({"seq": 42, "kind": "sample_record", "labels": ["alpha", "beta", "gamma", "delta", "epsilon"],
+                      "stats": {"ok": True, "values": [12, 240, 3600, 48000, 510000]},
+                      "note": "One small record, repeated until the buffer is full, compresses very well."},
+                     separators=(",", ":"))
+    out = []
+    for n in (1 << 16, 1 << 20, 4 << 20):
+        raw = np.frombuffer((rec * (n // len(rec) + 1)).encode()[:n], dtype=np.uint8)
+        out.append((O.compress_block_bytes(raw), raw))
+    return out
+
+
+@pytest.mark.gpu
+def test_json_repeat_reference_mode_matches_reference_decoder():
+    lz4mi = pytest.importorskip("lz4mi")
+    lz4mi.init(0)
+    cases = json_blocks()
+    comps = [c for c, _ in cases]
+    sizes = [r.size for _, r in cases]
+    refs = [O.decompress_block(c, n, js_compat=True) for c, n in zip(comps, sizes)]
+    assert any(not np.array_equal(r[2], raw) for r, (_, raw) in zip(refs, cases))   # the reference corrupts it (F1)
+    st, outs, _ = lz4mi.decompress_blocks(comps, sizes, js_exact=True)          # batched, in-kernel replay
+    for k, o, r in zip(st, outs, refs):
+        assert k == r[0] and np.array_equal(o, r[2])
+    for c, n, r in zip(comps, sizes, refs):                                     # one block per call
+        st1, outs1, _ = lz4mi.decompress_blocks([c], [n], js_exact=True)
+        assert st1[0] == r[0] and np.array_equal(outs1[0], r[2])
+    st, outs, _ = lz4mi.decompress_blocks(comps, sizes)                          # spec
+    for k, o, (_, raw) in zip(st, outs, cases):
+        assert k == 0 and np.array_equal(o, raw)
+

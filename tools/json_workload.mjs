@@ -1,0 +1,37 @@
+// The reference's own published benchmark, run through the drop-in: LZ4.compress /
+// LZ4.decompress of JSON text made of one small record repeated (the shape of
+// benchmark/src/base/benchUtils.js's data; our own record), 4 MiB independent blocks,
+// no checksum (benchmark/src/base/benchWorker.js:47-54), host buffers through N-API.
+// Rates in MB/s with MB = 2^20 bytes, as the reference's docs/BENCHMARKS.md reports them.
+//   node tools/json_workload.mjs [MiB] [reps]
+// Prints one JSON line.
+import { LZ4 } from '../divortio-lz4_amd/js/lz4mi.mjs';
+import { jsonRepeat } from './json_data.mjs';
+
+if (import.meta.url === `file://${process.argv[1]}`) {
+    const mib = Number(process.argv[2] || 25);
+    const reps = Number(process.argv[3] || 5);
+    const input = jsonRepeat(mib << 20);
+    const now = () => Number(process.hrtime.bigint()) / 1e9;
+    const rate = (fn) => {
+        fn();                                   // warm-up (device init, scratch growth)
+        const t0 = now();
+        for (let r = 0; r < reps; r++) fn();
+        return +(input.length * reps / (now() - t0) / (1 << 20)).toFixed(1);
+    };
+    const out = { bytes: input.length, block_size: 4194304 };
+    let frame = LZ4.compress(input, null, 4194304, true, false);
+    out.ratio = +(input.length / frame.length).toFixed(1);
+    out.compress_MBps = rate(() => { frame = LZ4.compress(input, null, 4194304, true, false); });
+    for (const mode of ['spec', 'reference']) {
+        LZ4.setDecodeMode(mode);
+        const back = LZ4.decompress(frame);
+        const same = Buffer.compare(Buffer.from(back), Buffer.from(input)) === 0;
+        if (mode === 'spec' && !same) throw new Error('spec round trip mismatch');
+        out[`${mode}_round_trip_exact`] = same;
+        out[`decompress_${mode}_MBps`] = rate(() => LZ4.decompress(frame));
+    }
+    LZ4.setDecodeMode('reference');
+    out.roundtrip_MBps = rate(() => LZ4.decompress(LZ4.compress(input, null, 4194304, true, false)));
+    console.log(JSON.stringify(out));
+}
