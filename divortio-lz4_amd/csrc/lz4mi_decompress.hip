@@ -934,6 +934,11 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         uint32_t vis, tail;
         {
         PROF(0);
+        // Wave priorities by phase (the 4 waves of a SIMD are in different phases):
+        // output rounds 3 > walks 1 > next-token table 0. The copies' loads and
+        // stores go out first and the LDS-bound parse fills the gaps: tiles216 -0.9 %,
+        // mix -2.5 %, copy -1.5 % (A/B in one process, profiles/r02j/prio_ab.json).
+        __builtin_amdgcn_s_setprio(0);
         // ---- 2. next-token table -----------------------------------------
         uint16_t* nxt = S.nxt;
         {   // all positions' fields read at once; the rare longer length fields afterwards
@@ -974,6 +979,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #endif
 
         PROF(1);
+        __builtin_amdgcn_s_setprio(1);
         // ---- 3. speculative walks + certification -------------------------
         uint32_t x;
         vis = 0;
@@ -1147,6 +1153,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
+        __builtin_amdgcn_s_setprio(3);
         // ---- 5. output rounds ---------------------------------------------
         // The previous chunk's stores (read back as history below) and the next
         // chunk's loads are complete: the stores had the whole parse to drain.
