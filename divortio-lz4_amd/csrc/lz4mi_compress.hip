@@ -691,6 +691,10 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
     wait_vmem();                 // the table is zero before the first exchange
     while (i < mflimit) {
         // ---- the probe at i: one exchange, then verification + speculative extension windows
+        // high wave priority on the chain (probe, hit test, extension); the previous
+        // sequence's emission below, off the chain, runs at low priority while its loads
+        // are in flight: tiles216 -2.1 % (A/B in one process, profiles/r02j/compress_prio_ab.json)
+        __builtin_amdgcn_s_setprio(3);
         const int32_t off0 = i - wb;
         uint32_t seq0;
         if (off0 >= 0 && off0 + 4 <= 4 * kWave) {
@@ -716,7 +720,9 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
             aw = ld_u32(j, (int64_t)i + 4 + 4 * lane);
             bw = ld_u32(j, (int64_t)cand0 + 4 + 4 * lane);
             if (pv) {
+                __builtin_amdgcn_s_setprio(0);
                 emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
+                __builtin_amdgcn_s_setprio(3);
                 pv = false;
             }
             hit0 = uniform(vw) == seq0;
