@@ -112,6 +112,11 @@ __device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int6
     if (lane < t) put_byte(j, d + 4 * nw + lane, src_byte(j, s + 4 * nw + lane));
 }
 
+// Value of v in lane l, l uniform (a ballot's ctz, a lane count): v_readlane
+// instead of the LDS permute __shfl compiles to (on the chain's critical path).
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int32_t lane_val(int32_t v, int l) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, l); }
+
 __device__ __forceinline__ uint32_t ld_u32(const CompJob& j, int64_t p) {
     if (p >= 0 && (uint64_t)p + 4 <= j.src_total) {
         uint32_t v;
@@ -143,8 +148,8 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
                 const uint64_t m = __ballot((x[u].x | x[u].y | x[u].z | x[u].w) != 0);
                 if (m) {
                     const int fl = __builtin_ctzll(m);
-                    const uint32_t w0 = __shfl(x[u].x, fl, kWave), w1 = __shfl(x[u].y, fl, kWave);
-                    const uint32_t w2 = __shfl(x[u].z, fl, kWave), w3 = __shfl(x[u].w, fl, kWave);
+                    const uint32_t w0 = lane_val(x[u].x, fl), w1 = lane_val(x[u].y, fl);
+                    const uint32_t w2 = lane_val(x[u].z, fl), w3 = lane_val(x[u].w, fl);
                     const int k = w0 ? 0 : w1 ? 4 : w2 ? 8 : 12;
                     const uint32_t wf = w0 ? w0 : w1 ? w1 : w2 ? w2 : w3;
                     const int64_t f = base + 16 * (fl + kWave * u) + k + (__builtin_ctz(wf) >> 3);
@@ -158,7 +163,7 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
         const uint64_t m = __ballot(x != 0);
         if (m) {
             const int fl = __builtin_ctzll(m);
-            const uint32_t xf = __shfl(x, fl, kWave);
+            const uint32_t xf = lane_val(x, fl);
             const int64_t f = base + 4 * fl + (__builtin_ctz(xf) >> 3);
             return f < lim ? f : lim;
         }
@@ -553,7 +558,7 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
         CPROF(1);
         // verification loads, and (speculating that the first probe hits) the
         // 256-byte extension windows of lane 0's candidate, in one round trip
-        const int32_t c0 = __shfl(cand, 0, kWave);
+        const int32_t c0 = lane_val(cand, 0);
         const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
         uint32_t aw = 0, bw = 0;
         if (c0 >= 0) {
@@ -594,14 +599,14 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
             atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
         }
         if (!hm) {
-            i = __shfl(p + (int32_t)step, nb - 1, kWave);
+            i = lane_val(p + (int32_t)step, nb - 1);
             c += nb;
             continue;
         }
         CPROF(4);
         CPROF_COUNT(9, 1);
         const int m = nprobe - 1;
-        const int32_t pm = __shfl(p, m, kWave), cm = __shfl(cand, m, kWave);
+        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
         c = 67;
         const int32_t lim = matchlimit - (pm + 4);
         int32_t f;
@@ -610,7 +615,7 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
             const uint64_t xm = __ballot(x != 0);
             if (xm) {
                 const int fl = __builtin_ctzll(xm);
-                f = 4 * fl + (__builtin_ctz((uint32_t)__shfl(x, fl, kWave)) >> 3);
+                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
             } else {
                 f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, pm + 4 + 4 * kWave,
                                                                         cm + 4 + 4 * kWave, lim - 4 * kWave)
@@ -735,7 +740,7 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
             int32_t f;
             if (xm) {
                 const int fl = __builtin_ctzll(xm);
-                f = 4 * fl + (__builtin_ctz((uint32_t)__shfl(x, fl, kWave)) >> 3);
+                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
             } else {
                 f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, i + 4 + 4 * kWave,
                                                                         cand0 + 4 + 4 * kWave, lim - 4 * kWave)
@@ -803,12 +808,12 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
         wait_vmem();                                           // ... before the next table access
         if (!hm) {
-            i = __shfl(p + (int32_t)step, nb - 1, kWave);
+            i = lane_val(p + (int32_t)step, nb - 1);
             c += nb;
             continue;
         }
         const int m = nprobe - 1;
-        const int32_t pm = __shfl(p, m, kWave), cm = __shfl(cand, m, kWave);
+        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
         c = 67;
         const int32_t e = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
         pv = true;
