@@ -44,16 +44,48 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-blocks", type=int, default=64, help="4 MiB blocks per CPU thread (pure-JS baseline)")
     ap.add_argument("--napi", type=int, default=1, help="time the JS drop-in end to end (host buffers)")
-    ap.add_argument("--frame-steps", type=int, default=3, help="time frame assembly (records + gather to rank 0)")
+    ap.add_argument("--frame-blocks", type=int, default=2048,
+                    help="4 MiB blocks per rank in the sharded frame workload (configs[3]; 0 = skip)")
     return ap.parse_args()
+
+
+def visible_gpus():
+    """GPUs this process may use, counted without touching HIP: the KFD topology's GPU
+    nodes (simd_count > 0) whose render node this user can open, limited by
+    HIP/ROCR/CUDA_VISIBLE_DEVICES when one is set."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        nodes = []
+    for d in nodes:
+        props = {}
+        try:
+            with open(os.path.join(base, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.strip().partition(" ")
+                    props[k] = v
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is None or os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            n += 1
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def launch_ranks(args):
     """--gpus N without a distributed environment: one process per GPU via
-    torch.distributed.run (started before this process touches the GPU)."""
+    torch.distributed.run. This process never initialises HIP (the GPUs are counted
+    from the KFD topology), so the ranks are its children, not a re-exec."""
     import socket
-    import torch
-    have = torch.cuda.device_count()          # does not initialise the GPU on this image
+    have = visible_gpus()
     if have < args.gpus:
         print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
         sys.exit(2)
@@ -154,56 +186,64 @@ def timed(torch, dist, fn, steps, warmup, stream_obj):
     return wall, kern
 
 
-def frame_assembly(torch, dist, lz4mi, batch, stream, stream_obj, steps, world):
-    """Frame records of every rank's blocks concatenated on rank 0:
-    record sizes + exclusive scan + lz4mi_frame_pack on each GPU, then (N>1) the
-    byte-count all-gather and point-to-point sends to rank 0 over RCCL. Reported
-    beside `value`, which stays the kernel-only decode rate."""
-    from lz4mi import shard
-    rec = shard.record_sizes(batch.comp_len, batch.raw_len)
-    total = int(rec.sum().item())
-    tot = torch.tensor([total], dtype=torch.int64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    if int(tot.item()) > (96 << 30):
-        return {"skipped": "gathered frame would exceed 96 GiB on rank 0"}
-    records = torch.empty(max(1, total), dtype=torch.uint8, device="cuda")
-    got = [None]
-
-    def step():
-        r = shard.record_sizes(batch.comp_len, batch.raw_len)
-        off = torch.cumsum(r, 0) - r
-        lz4mi.frame_pack_dev(batch.raw.data_ptr(), batch.raw_off.data_ptr(), batch.raw_len.data_ptr(),
-                             batch.comp.data_ptr(), batch.comp_off.data_ptr(), batch.comp_len.data_ptr(),
-                             records.data_ptr(), off.data_ptr(), batch.n, stream)
-        if dist is not None:
-            got[0] = shard.gather_records_to_root(records[:total], root=0)
-
-    wall, kern = timed(torch, dist, step, steps, 1, stream_obj)
-    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t[0])
-    # check: the first record's size word on rank 0 == this rank's first record
-    ok = True
-    if got[0] is not None:
-        ok = bool(torch.equal(got[0][:4], records[:4])) and got[0].numel() == int(tot.item())
-    # the frame's content checksum is one serial XXH32 chain over all raw bytes (SURVEY F5): its host
-    # rate (streaming state, 64-bit length) on a 256 MiB sample of this rank's raw blocks
-    sample = batch.raw[:min(batch.n, 64) * BLOCK].cpu().numpy()
-    h = lz4mi.XXHash32(0, len64=True)
+def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank):
+    """BASELINE.json configs[3]: one LZ4 frame (independent 4 MiB blocks, content size and
+    content checksum: FLG 0x6C, BD 0x70) over every rank's tiles216 shard, assembled on rank 0,
+    then decoded with its blocks shared out again (lz4mi.frame). 2048 blocks per rank make
+    the 64 GiB frame of configs[3] at 8 GPUs. Each phase is closed by a barrier and reported
+    separately: kernel only, + collective, + content checksum, end to end."""
+    from lz4mi import frame as F
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = blocks_per_rank
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device=dev)
+    lz4mi.generate_blocks_dev(raw.data_ptr(), "tiles216", 1 + rank * n, BLOCK, n, stream_obj.cuda_stream)
+    torch.cuda.synchronize()
+    codec = F.DeviceCodec(stream_obj)
+    tc = {}
     t0 = time.perf_counter()
-    h.update(sample)
-    h.digest()
-    xxh_gbps = sample.size / (time.perf_counter() - t0) / 1e9
-    return {"record_GBps": round(int(tot.item()) * steps / wall / 1e9, 2),
-            "content_checksum_host_GBps": round(xxh_gbps, 2),
-            "content_checksum_note": "one host core (the chain is serial); the sharded-frame path "
-                                     "(lz4mi.frame) overlaps it with the record gather",
-            "note": "frame record bytes (size words + payloads) packed and gathered per second",
-            "ms_per_step": round(wall / steps * 1e3, 3), "record_bytes": int(tot.item()),
-            "collective": "all_gather(sizes) + send/irecv to rank 0" if dist is not None else None,
-            "consistent": ok}
+    frame = F.compress_frame_sharded(raw, BLOCK, content_checksum=True, add_content_size=True, codec=codec, timings=tc)
+    c_total = time.perf_counter() - t0
+    fbytes = torch.tensor([frame.numel() if frame is not None else 0], dtype=torch.int64, device=dev)
+    if dist is not None:
+        dist.all_reduce(fbytes)
+    td = {}
+    t0 = time.perf_counter()
+    out = F.decompress_frame_sharded(frame, verify_checksum=True, decoder=F.DeviceDecoder(stream_obj), timings=td,
+                                     device=dev)
+    d_total = time.perf_counter() - t0
+    total_raw = world * n * BLOCK
+    ok = torch.tensor([1], dtype=torch.int32, device=dev)
+    if rank == 0:   # the checksum inside the decode checked every byte; the root's own shard once more
+        ok[0] = int(out.numel() == total_raw and bool(torch.equal(out[:n * BLOCK], raw)))
+    if dist is not None:
+        dist.broadcast(ok, src=0)
+    del out, frame, raw
+    torch.cuda.empty_cache()
+    ms = lambda v: round(v * 1e3, 2)
+    gbps = lambda v: round(total_raw / v / 1e9, 2) if v > 0 else None
+    ck = tc.get("kernel", 0.0)
+    ckc = ck + tc.get("collective", 0.0)
+    ckcs = ckc + tc.get("checksum", 0.0)
+    dk = td.get("kernel", 0.0)
+    dkc = dk + td.get("index", 0.0) + td.get("scatter", 0.0) + td.get("gather", 0.0)
+    dkcs = dkc + td.get("checksum", 0.0)
+    return {
+        "workload": f"LZ4 frame (independent 4 MiB blocks, content size + content xxh32), {n} tiles216 blocks "
+                    f"per rank x {world} rank(s) = {total_raw / 2**30:.0f} GiB; assembled on rank 0, then decoded "
+                    f"sharded (contiguous block runs) and gathered back to rank 0 (BASELINE.json configs[3])",
+        "raw_bytes": total_raw, "frame_bytes": int(fbytes.item()), "verified": bool(ok.item()),
+        "compress": {"kernel_ms": ms(ck), "kernel_collective_ms": ms(ckc), "kernel_collective_checksum_ms": ms(ckcs),
+                     "end_to_end_ms": ms(c_total), "phases_ms": {k: ms(v) for k, v in tc.items()},
+                     "kernel_GBps": gbps(ck), "kernel_collective_GBps": gbps(ckc),
+                     "kernel_collective_checksum_GBps": gbps(ckcs), "end_to_end_GBps": gbps(c_total)},
+        "decompress": {"kernel_ms": ms(dk), "kernel_collective_ms": ms(dkc), "kernel_collective_checksum_ms": ms(dkcs),
+                       "end_to_end_ms": ms(d_total), "phases_ms": {k: ms(v) for k, v in td.items()},
+                       "kernel_GBps": gbps(dk), "kernel_collective_GBps": gbps(dkc),
+                       "kernel_collective_checksum_GBps": gbps(dkcs), "end_to_end_GBps": gbps(d_total)},
+        "collective": ("all_gather(byte counts) + send/recv of records to rank 0; decode: broadcast of the block "
+                       "index, send of each rank's frame bytes, send/recv of outputs to rank 0") if world > 1 else None,
+        "checksum": "serial XXH32 on rank 0's host over host-staged shards (/dev/shm), one core",
+    }
 
 
 def cpu_threads():
@@ -350,8 +390,6 @@ def main():
 
     d_wall, d_kern = timed(torch, dist, lambda: batch.decompress(lz4mi, stream), args.steps, args.warmup, stream_obj)
     ok = batch.verify(torch, lz4mi, stream)
-    frame = frame_assembly(torch, dist, lz4mi, batch, stream, stream_obj, args.frame_steps, world) \
-        if args.frame_steps > 0 else None
 
     t = torch.tensor([d_wall, c_wall], dtype=torch.float64, device="cuda")
     okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device="cuda")
@@ -386,6 +424,14 @@ def main():
             torch.cuda.empty_cache()
         batch.dec = torch.empty(1, dtype=torch.uint8, device="cuda")
 
+    frame = None
+    if args.frame_blocks > 0:
+        del batch
+        torch.cuda.empty_cache()
+        try:
+            frame = frame_workload(torch, dist, lz4mi, stream_obj, world, rank, args.frame_blocks)
+        except Exception as e:    # reported, not fatal: every rank raises the same error (lz4mi.frame)
+            frame = {"error": repr(e)[-500:]}
     achieved = (raw_bytes + comp_bytes) / d_kern / 1e9
     traffic, traffic_src = pmc_traffic(lz4mi, n, args.gen)
     line = {

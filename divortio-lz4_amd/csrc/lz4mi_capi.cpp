@@ -24,10 +24,6 @@
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
                                               int32_t*, uint32_t, int, hipStream_t);
-extern "C" hipError_t lz4mi_launch_decompress_pending(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
-                                                      const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
-                                                      uint32_t*, int32_t*, uint32_t, const uint64_t*, const uint32_t*,
-                                                      hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
@@ -41,6 +37,8 @@ extern "C" hipError_t lz4mi_launch_generate(uint8_t*, uint32_t, uint32_t, uint32
 extern "C" hipError_t lz4mi_launch_frame_scan(const uint8_t*, uint64_t, uint32_t, uint64_t*, uint32_t*, uint64_t*,
                                               uint32_t*, uint64_t*, uint32_t*, uint64_t*, uint32_t*, uint32_t*,
                                               int64_t*, hipStream_t);
+extern "C" hipError_t lz4mi_launch_frame_index(const uint8_t*, uint64_t, uint32_t, uint64_t*, uint32_t*, int64_t*,
+                                               hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_stored(const uint8_t*, uint64_t, const uint64_t*, const uint32_t*,
                                                 const uint64_t*, uint8_t*, uint64_t, uint32_t, hipStream_t);
 
@@ -70,25 +68,21 @@ struct Scratch {
 };
 
 // Scratch of the work enqueued on one stream: kernels on one stream run in
-// order, so reusing it needs no lock or event; different streams never share.
+// order, so the device never sees two users of it at once; different streams
+// never share. Host threads can still call in on the same stream (the NULL
+// stream is torch's default), so `mu` is held from the first ensure() of a call
+// until its last launch that uses the scratch: a concurrent grow cannot free a
+// buffer another thread has read but not yet enqueued.
 struct StreamCtx {
     hipStream_t stream = nullptr;
+    std::mutex mu;
     Scratch tables;       // batch encoder hash tables (64 KiB per block)
-    Scratch chunk_base;   // two-pass decoder: first bitmap chunk of each block (device plan)
-    Scratch bitmap;       // token bitmaps, 128 B per 1 KiB compressed chunk
     Scratch frame_meta;   // block-checksum payload offsets / lengths of frame_pack
     Scratch scan;         // frame_decompress: block lists of the device frame walk
-    uint64_t bitmap_chunks = 0;
-    uint32_t* needed = nullptr;   // host-mapped: chunks the last plan wanted (read lazily)
     void release() {
         tables.release();
-        chunk_base.release();
-        bitmap.release();
         frame_meta.release();
         scan.release();
-        if (needed) (void)hipHostFree(needed);
-        needed = nullptr;
-        bitmap_chunks = 0;
     }
 };
 
@@ -111,13 +105,28 @@ std::mutex g_init_mu;
         if (e_ != hipSuccess) return LZ4MI_ERR_HIP; \
     } while (0)
 
-int32_t ensure_init() {
-    if (g_ctx.device >= 0) {
-        // HIP's current device is per host thread: callers may come from any thread
-        return hipSetDevice(g_ctx.device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
+// Every entry point runs on the library's device and leaves the calling thread's
+// current device as it found it (HIP's current device is per host thread, and
+// torch allocates on it).
+class DeviceGuard {
+  public:
+    DeviceGuard() {
+        if (g_ctx.device < 0) {
+            status_ = lz4mi_init(-1);
+            if (status_) return;
+        }
+        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+        if (prev_ != g_ctx.device && hipSetDevice(g_ctx.device) != hipSuccess) status_ = LZ4MI_ERR_HIP;
     }
-    return lz4mi_init(-1);
-}
+    ~DeviceGuard() {
+        if (prev_ >= 0 && prev_ != g_ctx.device) (void)hipSetDevice(prev_);
+    }
+    int32_t status() const { return status_; }
+
+  private:
+    int prev_ = -1;
+    int32_t status_ = LZ4MI_OK;
+};
 
 // Device-pointer calls run on the caller's stream; NULL is HIP's default stream (what
 // torch reports for its default stream), so work is ordered with the caller's kernels.
@@ -132,83 +141,9 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
-constexpr uint64_t kBitmapChunks0 = 1u << 19;   // initial bitmap capacity: 512 Ki chunks = 64 MiB
-
-// Decoder selection (LZ4MI_DECODER): "single" (default) = the single-pass kernel for
-// every block (with long periodic runs written from LDS it is the faster decoder on
-// every generator measured); "ring" = every block through the
-// two-pass ring decoder; "auto" = the ring decoder for blocks compressed at least
-// kRingRatio:1, the single-pass kernel for the rest (the round-1 dispatch).
-constexpr uint32_t kRingRatio = 32;
-int g_ring_mode = -1;
-uint32_t g_ring_ratio = kRingRatio;
-bool ring_enabled() {
-    if (g_ring_mode < 0) {
-        const char* e = std::getenv("LZ4MI_DECODER");
-        const bool ring = e && std::strcmp(e, "ring") == 0, autom = e && std::strcmp(e, "auto") == 0;
-        g_ring_mode = (ring || autom) ? 1 : 0;
-        g_ring_ratio = ring ? 0u : kRingRatio;
-    }
-    return g_ring_mode == 1;
-}
-
-// Spec-mode decode of a batch whose pointers are all device pointers: a
-// device-side plan (which blocks the two-pass ring decoder takes, their bitmap
-// chunks), pass 1 + pass 2 of the ring decoder, then the single-pass kernel for
-// every other block. Nothing is read back: the call only enqueues. The bitmap
-// scratch is sized from what earlier plans on this stream needed (a host-mapped
-// word the plan writes); blocks that do not fit this call's scratch simply go to
-// the single-pass kernel.
-hipError_t ring_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
-                       const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
-                       uint32_t* out_len, int32_t* status, uint32_t nblocks, hipStream_t s) {
-    StreamCtx* c = stream_ctx(s);
-    hipError_t e;
-    if (!c->needed) {
-        if ((e = hipHostMalloc((void**)&c->needed, 64, hipHostMallocMapped)) != hipSuccess) return e;
-        *c->needed = 0;
-    }
-    uint64_t want = std::max<uint64_t>(kBitmapChunks0, (uint64_t)*c->needed);
-    uint64_t limit = UINT64_MAX;
-    if (const char* cap = std::getenv("LZ4MI_RING_MAX_CHUNKS")) {   // tests: a small scratch forces overflow
-        limit = std::strtoull(cap, nullptr, 10);
-        want = limit;
-    }
-    if (want > c->bitmap_chunks) {
-        if ((e = c->bitmap.ensure(want * 128 + 64, s)) != hipSuccess) return e;
-        c->bitmap_chunks = (c->bitmap.cap - 64) / 128;
-    }
-    const uint64_t capacity = std::min<uint64_t>(c->bitmap_chunks, limit);
-    if ((e = c->chunk_base.ensure(4ull * nblocks + 64, s)) != hipSuccess) return e;
-    uint32_t* needed_dev = nullptr;
-    if ((e = hipHostGetDevicePointer((void**)&needed_dev, c->needed, 0)) != hipSuccess) return e;
-    uint32_t* stats = nullptr;
-    if (std::getenv("LZ4MI_RING_STATS")) {
-        if (!g_ctx.stats.p) {
-            if ((e = g_ctx.stats.ensure(64, s)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(g_ctx.stats.p, 0, 64, s)) != hipSuccess) return e;
-        }
-        stats = g_ctx.stats.as<uint32_t>();
-    }
-    if ((e = lz4mi_launch_ring_plan(in_len, out_cap, g_ring_ratio, nblocks, capacity,
-                                    c->chunk_base.as<uint32_t>(), needed_dev, s)) != hipSuccess)
-        return e;
-    if ((e = lz4mi_launch_token_map(in, in_off, in_len, out_cap, g_ring_ratio, c->chunk_base.as<uint32_t>(),
-                                    c->bitmap.as<uint64_t>(), nblocks, s)) != hipSuccess)
-        return e;
-    if ((e = lz4mi_launch_ring_decode(in, in_off, in_len, out, out_off, out_cap, out_len, status,
-                                      c->chunk_base.as<uint32_t>(), c->bitmap.as<uint64_t>(), g_ring_ratio, stats,
-                                      nblocks, s)) != hipSuccess)
-        return e;
-    return lz4mi_launch_decompress_pending(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
-                                           nblocks, nullptr, nullptr, s);
-}
-
 hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s) {
-    if (mode == 0 && ring_enabled())
-        return ring_decode(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks, s);
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
                                    nblocks, mode, s);
 }
@@ -281,33 +216,6 @@ const char* lz4mi_status_message(int32_t s) {
     }
 }
 
-// Debug counters of the two-pass decoder (enabled by LZ4MI_RING_STATS=1):
-// [0] chunks whose token bitmap was rebuilt, [1] sequences written directly,
-// [2] blocks handed to the single-pass kernel. Reads and resets.
-// [3..5] why blocks were handed back: malformed token, sequence error, direct-sequence error.
-int32_t lz4mi_debug_ring_stats(uint32_t* out6) {
-    for (int i = 0; i < 6; ++i) out6[i] = 0;
-    if (!g_ctx.stats.p) return LZ4MI_OK;
-    if (hipDeviceSynchronize() != hipSuccess) return LZ4MI_ERR_HIP;
-    if (hipMemcpy(out6, g_ctx.stats.p, 24, hipMemcpyDeviceToHost) != hipSuccess) return LZ4MI_ERR_HIP;
-    if (hipMemset(g_ctx.stats.p, 0, 24) != hipSuccess) return LZ4MI_ERR_HIP;
-    return LZ4MI_OK;
-}
-
-// Decoder selection for tests / tools: mode 0 single-pass only, 1 ring decoder for blocks
-// compressed at least `ratio`:1 (0: every block), -1 back to LZ4MI_DECODER's choice.
-// Overrides LZ4MI_DECODER.
-int32_t lz4mi_debug_set_decoder(int32_t mode, uint32_t ratio) {
-    if (mode < 0) {
-        g_ring_mode = -1;
-        ring_enabled();
-        return LZ4MI_OK;
-    }
-    g_ring_mode = mode ? 1 : 0;
-    g_ring_ratio = ratio;
-    return LZ4MI_OK;
-}
-
 const char* lz4mi_version(void) { return "lz4mi 0.2 (gfx950) src " LZ4MI_SRC_HASH; }
 
 const char* lz4mi_build_id(void) { return LZ4MI_SRC_HASH; }
@@ -318,19 +226,31 @@ int32_t lz4mi_device_count(void) {
     return n;
 }
 
+static int32_t init_locked(int32_t device);
+
+// Selects (and on first use sets up) the library's device; the calling thread's
+// current device is restored before returning.
 int32_t lz4mi_init(int32_t device) {
     std::lock_guard<std::mutex> lk(g_init_mu);
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    const int32_t st = init_locked(device);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return st;
+}
+
+static int32_t init_locked(int32_t device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return LZ4MI_ERR_NO_DEVICE;
     if (device < 0) {
-        if (g_ctx.device >= 0) return hipSetDevice(g_ctx.device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
+        if (g_ctx.device >= 0) return LZ4MI_OK;
         if (hipGetDevice(&device) != hipSuccess) device = 0;
     }
     if (device >= n) return LZ4MI_ERR_ARG;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return LZ4MI_ERR_HIP;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LZ4MI_ERR_NO_DEVICE;
-    if (g_ctx.device == device) return hipSetDevice(device) == hipSuccess ? LZ4MI_OK : LZ4MI_ERR_HIP;
+    if (g_ctx.device == device) return LZ4MI_OK;
     if (g_ctx.device >= 0) {
         // switching devices: every buffer of the old context lives on the old device
         std::lock_guard<std::mutex> lk2(g_ctx.mu);
@@ -420,8 +340,8 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
                                 const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
                                 uint32_t dict_len, uint32_t* out_len, int32_t* status, uint32_t nblocks,
                                 uint32_t flags, void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     const int js = (flags & LZ4MI_JS_COMPAT) ? 1 : 0;
     const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
     if (nblocks == 0) return LZ4MI_OK;
@@ -506,13 +426,14 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
 int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                               const uint64_t* out_off, uint32_t* out_len, uint32_t nblocks, uint32_t flags,
                               void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
         // the hash-table scratch belongs to the stream: kernels of one stream use it in order
         hipStream_t s = pick_stream(stream);
         StreamCtx* c = stream_ctx(s);
+        std::lock_guard<std::mutex> sl(c->mu);
         LZ4MI_TRY(c->tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t), s));
         LZ4MI_TRY(lz4mi_launch_compress(in, in_off, in_len, out, out_off, out_len, nblocks, c->tables.as<int32_t>(), s));
         return LZ4MI_OK;
@@ -544,6 +465,7 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
     StreamCtx* c = stream_ctx(s);
+    std::unique_lock<std::mutex> sl(c->mu);
     LZ4MI_TRY(c->tables.ensure((size_t)nblocks * 16384 * sizeof(int32_t), s));
     LZ4MI_TRY(lz4mi_launch_compress(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off,
                                     m_out_len, nblocks, c->tables.as<int32_t>(), s));
@@ -560,8 +482,8 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
 int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
                                    int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off, uint32_t flags,
                                    void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table)
         return LZ4MI_ERR_ARG;
     if (out_off < 0) return LZ4MI_ERR_ARG;
@@ -600,8 +522,8 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
 
 int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,
                            uint32_t* hashes, uint32_t nblocks, uint32_t flags, void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     const int stdv = (flags & LZ4MI_XXH_STANDARD) ? 1 : 0;
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
@@ -632,8 +554,8 @@ int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_
 int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len, const uint8_t* comp,
                          const uint64_t* comp_off, const uint32_t* comp_len, uint8_t* frame, const uint64_t* rec_off,
                          uint32_t nblocks, uint32_t flags, void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     if (!(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
     if (nblocks == 0) return LZ4MI_OK;
     hipStream_t s = pick_stream(stream);
@@ -646,6 +568,7 @@ int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint
     // payload's position and length, the batched XXH32 kernel hashes the payloads in place
     // and stores each digest after its payload
     StreamCtx* c = stream_ctx(s);
+    std::lock_guard<std::mutex> sl(c->mu);
     LZ4MI_TRY(c->frame_meta.ensure((size_t)nblocks * 20 + 64, s));
     uint64_t* pay_off = c->frame_meta.as<uint64_t>();
     uint64_t* sum_off = pay_off + nblocks;
@@ -658,8 +581,8 @@ int32_t lz4mi_frame_pack(const uint8_t* raw, const uint64_t* raw_off, const uint
 
 int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out, uint64_t out_cap, int64_t* info,
                                uint32_t flags, void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     if (!(flags & LZ4MI_DEVICE_PTRS) || !info || (flags & LZ4MI_JS_COMPAT)) return LZ4MI_ERR_ARG;
     for (int k = 0; k < 8; ++k) info[k] = 0;
     hipStream_t s = pick_stream(stream);
@@ -668,12 +591,28 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
     uint8_t h[19] = {0};
     LZ4MI_TRY(hipMemcpyAsync(h, frame, std::min<uint64_t>(len, 19), hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
+    // magic and version as the device walk reports them (bufferDecompress.js:59-67)
+    if (len < 4 || le32(h) != 0x184D2204u) {
+        info[0] = LZ4MI_ERR_MAGIC;
+        return LZ4MI_OK;
+    }
+    info[1] = len > 4 ? h[4] : 0;
+    if (((info[1] & 0xC0) >> 6) != 1) {
+        info[0] = LZ4MI_ERR_VERSION;
+        return LZ4MI_OK;
+    }
     const uint64_t size = (len >= 14 && (h[4] & 0x08)) ? (uint64_t)le32(h + 6) | ((uint64_t)le32(h + 10) << 32) : 0;
+    info[2] = (int64_t)size;
+    // no content size (or 0), or more than the caller's buffer: the host path decodes the frame;
+    // checked before any scratch is sized from the header's claim
+    if (size == 0 || size > out_cap) return LZ4MI_ERR_ARG;
     const uint32_t id = len > 5 ? (h[5] >> 4) & 7 : 7;
     const uint64_t bmax = id == 4 ? 65536 : id == 5 ? 262144 : id == 6 ? 1048576 : 4194304;
-    const uint64_t cap_blocks = size / bmax + 2;
+    // every record takes at least its 4-byte size word
+    const uint64_t cap_blocks = std::min<uint64_t>(size / bmax, len / 4) + 2;
     if (cap_blocks > 0xFFFFFFF0ull) return LZ4MI_ERR_ARG;
     StreamCtx* c = stream_ctx(s);
+    std::lock_guard<std::mutex> sl(c->mu);
     const size_t per = 8 + 4 + 8 + 4 + 4;   // compressed lists (in_off, in_len, out_off, out_cap, idx)
     const size_t per_s = 8 + 4 + 8 + 4;     // stored lists (in_off, len, out_off, idx)
     const size_t meta = cap_blocks * (per + per_s + 4 + 4) + 64 + 64;   // + out_len, status
@@ -754,10 +693,20 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
     return LZ4MI_OK;
 }
 
+int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off, uint32_t* size_word,
+                          uint32_t cap_blocks, int64_t* info, uint32_t flags, void* stream) {
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
+    if (!(flags & LZ4MI_DEVICE_PTRS) || !frame || !info || (cap_blocks && (!pay_off || !size_word)))
+        return LZ4MI_ERR_ARG;
+    LZ4MI_TRY(lz4mi_launch_frame_index(frame, len, cap_blocks, pay_off, size_word, info, pick_stream(stream)));
+    return LZ4MI_OK;
+}
+
 int32_t lz4mi_generate_blocks(uint8_t* out, uint32_t kind, uint32_t seed0, uint32_t block_size, uint32_t nblocks,
                               void* stream) {
-    int32_t st = ensure_init();
-    if (st) return st;
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
     if (kind > 2) return LZ4MI_ERR_ARG;
     LZ4MI_TRY(lz4mi_launch_generate(out, kind, seed0, block_size, nblocks, pick_stream(stream)));
     return LZ4MI_OK;

@@ -133,6 +133,54 @@ __global__ __launch_bounds__(64) void lz4mi_frame_scan_kernel(const uint8_t* f, 
     info[5] = (int64_t)pos; info[6] = bmax; info[7] = overflow;
 }
 
+// The frame's block index for sharded decoding (lz4mi_frame_index): one lane walks the
+// header and the size words like the scan above, and lists every block in frame order:
+// payload position and raw size word (stored bit 31 included). info as for the scan,
+// with [3] = blocks listed and [4] = 0.
+__global__ __launch_bounds__(64) void lz4mi_frame_index_kernel(const uint8_t* f, uint64_t len, uint32_t cap_blocks,
+                                                               uint64_t* pay_off, uint32_t* size_word, int64_t* info) {
+    if (threadIdx.x != 0) return;
+    auto rd = [&](uint64_t p) -> uint32_t {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) v |= (p + k < len ? (uint32_t)f[p + k] : 0u) << (8 * k);
+        return v;
+    };
+    int64_t st = 0, flg = 0, size = 0, nb = 0, overflow = 0;
+    uint64_t pos = 0;
+    int64_t bmax = 4194304;
+    if (len < 4 || rd(0) != 0x184D2204u) {
+        st = -5;
+    } else {
+        flg = len > 4 ? f[4] : 0;
+        if (((flg & 0xC0) >> 6) != 1) {
+            st = -6;
+        } else {
+            const uint32_t id = len > 5 ? (f[5] >> 4) & 7 : 7;
+            bmax = id == 4 ? 65536 : id == 5 ? 262144 : id == 6 ? 1048576 : 4194304;
+            pos = 6;
+            if (flg & 0x08) {
+                size = (int64_t)((uint64_t)rd(pos) | ((uint64_t)rd(pos + 4) << 32));
+                pos += 8;
+            }
+            if (flg & 0x01) pos += 4;
+            pos += 1;
+            while (pos < len) {
+                const uint32_t bs = rd(pos);
+                pos += 4;
+                if (bs == 0) break;
+                if (nb >= (int64_t)cap_blocks) { overflow = 1; break; }
+                pay_off[nb] = pos;
+                size_word[nb] = bs;
+                ++nb;
+                pos += (uint64_t)(bs & 0x7FFFFFFFu) + ((flg & 0x10) ? 4 : 0);
+            }
+            if (pos > len) overflow = 1;
+        }
+    }
+    info[0] = st; info[1] = flg; info[2] = size; info[3] = nb; info[4] = 0;
+    info[5] = (int64_t)pos; info[6] = bmax; info[7] = overflow;
+}
+
 // Stored blocks' bytes into the output (one wave per stored block; clipped at `cap`
 // like the reference's result.set would throw past it: the caller checks first).
 __global__ __launch_bounds__(64) void lz4mi_frame_stored_kernel(const uint8_t* f, uint64_t len, const uint64_t* s_in_off,
@@ -195,5 +243,12 @@ extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t* raw, const uint64_t
     if (nblocks == 0) return hipSuccess;
     hipLaunchKernelGGL(lz4mi::lz4mi_frame_pack_kernel, dim3(nblocks), dim3(64), 0, stream, raw, raw_off, raw_len,
                        comp, comp_off, comp_len, frame, rec_off, nblocks, pay_off, sum_off, pay_len);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t lz4mi_launch_frame_index(const uint8_t* f, uint64_t len, uint32_t cap_blocks, uint64_t* pay_off,
+                                               uint32_t* size_word, int64_t* info, hipStream_t stream) {
+    hipLaunchKernelGGL(lz4mi::lz4mi_frame_index_kernel, dim3(1), dim3(64), 0, stream, f, len, cap_blocks, pay_off,
+                       size_word, info);
     return hipGetLastError();
 }

@@ -25,6 +25,7 @@ const MAGIC = 0x184D2204;
 const HASH_TABLE_SIZE = 16384;
 const BLOCK_MAX_SIZES = { 4: 65536, 5: 262144, 6: 1048576, 7: 4194304 };
 const WINDOW_SIZE = 65536;
+const DECODE_BATCH_BYTES = 256 * 1024 * 1024;   // output slots per batched decode call (LZ4Decoder)
 
 // module-global table, as the reference's GLOBAL_HASH_TABLE (bufferCompress.js:56)
 const HASH_TABLE = new Int32Array(HASH_TABLE_SIZE);
@@ -650,8 +651,10 @@ export class LZ4Decoder {
         }
         const output = [];
         const pending = [];      // compressed blocks of an independent frame, decoded together
+        let pendingBytes = 0;    // their output slots (bounded: one batch <= DECODE_BATCH_BYTES)
         const flush = () => {
             if (pending.length === 0) return;
+            pendingBytes = 0;
             const dec = this._decodeIndependent(pending);
             for (let k = 0; k < pending.length; k++) {
                 if (pending[k].slot === null) continue;
@@ -671,6 +674,7 @@ export class LZ4Decoder {
             if (this.state === 1) {                                   // header
                 if (this.buffer.length < 2) break;
                 const flg = this.buffer[0];
+                this.blockMax = BLOCK_MAX_SIZES[(this.buffer[1] >> 4) & 7] || BLOCK_MAX_SIZES[7];
                 this.blockIndependence = (flg & 0x20) !== 0;
                 this.hasBlockChecksum = (flg & 0x10) !== 0;
                 const hasContentSize = (flg & 0x08) !== 0;
@@ -707,6 +711,8 @@ export class LZ4Decoder {
                 if (this.blockIndependence && !this.isUncompressed) {
                     pending.push({ data: blockData, slot: output.length });
                     output.push(null);
+                    pendingBytes += this.blockMax;
+                    if (pendingBytes >= DECODE_BATCH_BYTES) flush();
                 } else {
                     flush();
                     let dec;
@@ -743,9 +749,11 @@ export class LZ4Decoder {
         return output;
     }
 
-    // independent compressed blocks, each as decompressBlock(block, 0, n, workspace, 0) decodes it
+    // independent compressed blocks, each as decompressBlock(block, 0, n, workspace, 0) decodes it:
+    // batched into slots of the frame's block maximum (BD); a block that does not fit its slot
+    // (OUTPUT_TOO_SMALL) is decoded again alone into the reference's 4 MiB workspace below
     _decodeIndependent(blocks) {
-        const nb = blocks.length, cap = BLOCK_MAX_SIZES[7];
+        const nb = blocks.length, cap = this.blockMax || BLOCK_MAX_SIZES[7];
         let total = 0;
         for (const b of blocks) total += b.data.length;
         const input = new Uint8Array(total);
@@ -766,7 +774,7 @@ export class LZ4Decoder {
             if (status[k] === native.ERR_CROSS_BLOCK || status[k] !== 0) {
                 // a back-reference (or the F1 rewrite) before the block's start: decode it alone,
                 // into a fresh workspace, which also raises the reference's error if it has one
-                const ws = new Uint8Array(cap);
+                const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
                 const w = native.decompressBlock(blocks[k].data, 0, blocks[k].data.length, ws, 0, null, decodeFlags);
                 res.push(ws.slice(0, w));
             } else {

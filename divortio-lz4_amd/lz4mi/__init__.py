@@ -38,7 +38,7 @@ EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_ve
            "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
            "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
-           "lz4mi_frame_decompress")
+           "lz4mi_frame_decompress", "lz4mi_frame_index")
 
 
 class Lz4miError(RuntimeError):
@@ -93,6 +93,8 @@ def lib():
         L.lz4mi_frame_pack.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]
         L.lz4mi_frame_decompress.restype = ctypes.c_int32
         L.lz4mi_frame_decompress.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]
+        L.lz4mi_frame_index.restype = ctypes.c_int32
+        L.lz4mi_frame_index.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
         L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, _vp]
@@ -310,3 +312,10 @@ def frame_pack_dev(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, co
     _check(lib().lz4mi_frame_pack(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr,
                                   rec_off_ptr, nblocks, DEVICE_PTRS | (BLOCK_CHECKSUM if block_checksum else 0),
                                   stream or None))
+
+
+def frame_index_dev(frame_ptr, frame_len, pay_off_ptr, size_word_ptr, cap_blocks, info_ptr, stream=0):
+    """Block index of a device-resident frame (include/lz4mi.h lz4mi_frame_index): device
+    pointers, asynchronous on `stream`."""
+    _check(lib().lz4mi_frame_index(frame_ptr, frame_len, pay_off_ptr, size_word_ptr, cap_blocks, info_ptr,
+                                   DEVICE_PTRS, stream or None))

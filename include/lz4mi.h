@@ -204,6 +204,18 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
                                uint32_t flags, void* stream);
 
 /*
+ * Block index of a device-resident frame, for decoding its blocks on several devices
+ * (the block walk of bufferDecompress.js:133-192 without decoding): one lane walks the
+ * header and the size words and writes, per block in frame order, the payload position
+ * (pay_off) and the raw size word (size_word, bit 31 = stored). info (8 x int64, device)
+ * as lz4mi_frame_decompress's, with [3] = blocks listed, [7] = 1 when the walk ran past
+ * the frame or past cap_blocks. Device pointers only (LZ4MI_DEVICE_PTRS); asynchronous
+ * on `stream`. Replaces nothing in the reference (its frame loop is serial in one call).
+ */
+int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off, uint32_t* size_word,
+                          uint32_t cap_blocks, int64_t* info, uint32_t flags, void* stream);
+
+/*
  * Synthetic input generator (bench/test support, not a reference interface):
  * block b = generator `kind` with seed seed0 + b, block_size bytes each,
  * written to out[b * block_size ..] (device pointer, async on stream).

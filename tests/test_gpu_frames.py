@@ -7,7 +7,7 @@ checked against the pinned oracle (bit-exact).
   config 5  the 50/50 random/tiles216 mix, shuffled and clustered, compressed and
             decoded on the GPU, per-block digests against the oracle
   plus      compressRaw's RangeError/F7 semantics, block checksums, unaligned
-            device xxh32, two concurrent streams, the ring decoder's bitmap overflow
+            device xxh32, two concurrent streams
 """
 import os
 
@@ -177,8 +177,7 @@ def test_xxh32_device_unaligned_buffers():
 
 
 def test_two_streams_concurrently_bit_exact():
-    """Device-pointer calls on two streams at once: per-stream scratch (hash tables, ring
-    bitmaps) keeps both exact; no call blocks the host (the include/lz4mi.h contract)."""
+    """Device-pointer calls on two streams at once: per-stream scratch (hash tables) keeps both exact; no call blocks the host (the include/lz4mi.h contract)."""
     n = 24
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     jobs = []
@@ -215,25 +214,6 @@ def test_two_streams_concurrently_bit_exact():
         assert (d_st == 0).all() and torch.equal(dec, raw), kind
         host = raw[: 1 << 20].cpu().numpy()
         assert np.array_equal(comp[:int(c_len[0])].cpu().numpy(), O.compress_block_bytes(host)), kind
-
-
-def test_ring_decoder_bitmap_overflow_falls_back_exactly(monkeypatch):
-    """When the device plan cannot fit every ring-eligible block in the bitmap scratch, the
-    blocks past it go to the single-pass kernel: same bytes, no host round trip."""
-    monkeypatch.setenv("LZ4MI_RING_MAX_CHUNKS", "12")
-    n, bs = 8, 1 << 20                 # repetitive 1 MiB blocks: ~5 chunks each (4 KiB compressed)
-    raw = torch.empty(n * bs, dtype=torch.uint8, device="cuda")
-    lz4mi.generate_blocks_dev(raw.data_ptr(), "repetitive", 3, bs, n, _stream())
-    srcs = [raw[b * bs:(b + 1) * bs].cpu().numpy() for b in range(n)]
-    comps = [O.compress_block_bytes(x) for x in srcs]
-    lz4mi.lib().lz4mi_debug_set_decoder(1, 32)   # the round-1 dispatch: ring decoder for >= 32:1 blocks
-    try:
-        st, outs, _ = lz4mi.decompress_blocks(comps, [bs] * n)
-    finally:
-        lz4mi.lib().lz4mi_debug_set_decoder(-1, 0)
-    assert (st == 0).all()
-    for s, o in zip(srcs, outs):
-        assert np.array_equal(s, o)
 
 
 @pytest.mark.parametrize("kind", ["copy", "runs", "text", "tiles216"])
@@ -283,6 +263,14 @@ def test_frame_decompress_on_device_matches_reference():
             with pytest.raises(lz4mi.Lz4miError) as ei:
                 F.decompress_frame_device(dev, js_exact=True, verify_checksum=cs)
             assert ei.value.status == est
+    # frames the device walk declines go through the host-buffer path, same bytes: no content
+    # size (the rolling 64 KiB window layout), and the empty input's frame (content size 0)
+    for bs, indep in ((65536, False), (4194304, True)):
+        f = O.compress_frame(data, None, bs, indep, True, False)
+        got = F.decompress_frame_device(torch.from_numpy(f.copy()).cuda())
+        assert np.array_equal(got.cpu().numpy(), data), (bs, indep)
+    f = O.compress_frame(np.zeros(0, dtype=np.uint8), None, 65536, True, True, True)
+    assert F.decompress_frame_device(torch.from_numpy(f.copy()).cuda()).numel() == 0
     bad = torch.from_numpy(np.frombuffer(bytes(range(6)), dtype=np.uint8).copy()).cuda()
     with pytest.raises(lz4mi.Lz4miError) as ei:
         F.decompress_frame_device(bad)

@@ -117,23 +117,15 @@ def test_periodic_runs_single_pass(source):
     cases = crafted_blocks() if source == "crafted" else natural_blocks()
     comps = [c for c, _ in cases]
     exps = [e for _, e in cases]
-    try:
-        lz4mi.lib().lz4mi_debug_set_decoder(0, 0)   # single-pass kernel for every block
-        st, outs, lens = lz4mi.decompress_blocks(comps, [e.size for e in exps])
-        for i, (k, o, n, e) in enumerate(zip(st, outs, lens, exps)):
-            assert k == 0 and n == e.size, i
-            assert np.array_equal(o, e), i
-        for i, (c, e) in enumerate(zip(comps, exps)):   # reference decode (serial and in-kernel F1), one block per array
-            ref = O.decompress_block(c, e.size, js_compat=True)
-            for mode in ({"js_compat": True}, {"js_exact": True}):
-                st1, outs1, _ = lz4mi.decompress_blocks([c], [e.size], **mode)
-                assert st1[0] == ref[0] and np.array_equal(outs1[0], ref[2]), (i, mode)
-        lz4mi.lib().lz4mi_debug_set_decoder(1, 0)   # and the ring decoder, same blocks
-        st, outs, lens = lz4mi.decompress_blocks(comps, [e.size for e in exps])
-        for i, (k, o, e) in enumerate(zip(st, outs, exps)):
-            assert k == 0 and np.array_equal(o, e), i
-    finally:
-        lz4mi.lib().lz4mi_debug_set_decoder(-1, 0)
+    st, outs, lens = lz4mi.decompress_blocks(comps, [e.size for e in exps])
+    for i, (k, o, n, e) in enumerate(zip(st, outs, lens, exps)):
+        assert k == 0 and n == e.size, i
+        assert np.array_equal(o, e), i
+    for i, (c, e) in enumerate(zip(comps, exps)):   # reference decode (serial and in-kernel F1), one block per array
+        ref = O.decompress_block(c, e.size, js_compat=True)
+        for mode in ({"js_compat": True}, {"js_exact": True}):
+            st1, outs1, _ = lz4mi.decompress_blocks([c], [e.size], **mode)
+            assert st1[0] == ref[0] and np.array_equal(outs1[0], ref[2]), (i, mode)
 
 
 def json_blocks():

@@ -89,17 +89,28 @@ class _OracleCodec:
         return torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8))
 
 
-def _oracle_decode(comp, block_max):
-    import oracle as O
-    outs = []
-    for c, stored in comp:
-        if stored:
-            outs.append(np.asarray(c))
-        else:
-            st, w, out = O.decompress_block(c, block_max)
-            assert st == 0
-            outs.append(out[:w])
-    return outs
+class _OracleDecoder:
+    """Each rank's decoder stand-in on CPU (the GPU path is lz4mi.frame.DeviceDecoder): the
+    same interface, the oracle decoding each block of the rank's run of frame bytes."""
+
+    def decode(self, rng, pay_rel, word, block_max, last_cap):
+        import torch
+        import oracle as O
+        f = rng.numpy()
+        outs, status = [], []
+        nb = pay_rel.numel()
+        for b in range(nb):
+            p, w = int(pay_rel[b]), int(word[b])
+            n, cap = w & 0x7FFFFFFF, (block_max if b + 1 < nb else last_cap)
+            if w & 0x80000000:
+                outs.append(f[p:p + n])
+                status.append(0)
+            else:
+                st, m, out = O.decompress_block(f[p:p + n], cap)
+                outs.append(out[:m] if st == 0 else np.zeros(0, dtype=np.uint8))
+                status.append(st)
+        cat = np.concatenate(outs) if outs else np.zeros(0, dtype=np.uint8)
+        return torch.from_numpy(np.ascontiguousarray(cat)), torch.tensor(status, dtype=torch.int32)
 
 
 def _frame_worker(rank, world, port, q):
@@ -122,15 +133,31 @@ def _frame_worker(rank, world, port, q):
             nb = -(-data.size // bsize)
             lo, hi = shard.shard_range(nb, rank, world)
             mine = torch.from_numpy(data[lo * bsize:min(data.size, hi * bsize)].copy())
-            got = F.compress_frame_sharded(mine, bsize, True, True, bcs, codec=_OracleCodec())
+            tim = {}
+            got = F.compress_frame_sharded(mine, bsize, True, True, bcs, codec=_OracleCodec(), timings=tim)
             ref = O.compress_frame(data, None, bsize, True, True, True, block_checksum=bcs)
-            ok = True
+            ok = all(k in tim for k in ("kernel", "collective", "checksum", "assemble"))
             if rank == 0:
-                ok = got is not None and np.array_equal(got.numpy(), ref)
+                ok = ok and got is not None and np.array_equal(got.numpy(), ref)
             else:
-                ok = got is None
-            back = F.decompress_frame_sharded(ref, True, decode=_oracle_decode)
+                ok = ok and got is None
+            tim = {}
+            fr = torch.from_numpy(ref.copy()) if rank == 0 else None
+            back = F.decompress_frame_sharded(fr, True, decoder=_OracleDecoder(), timings=tim)
             ok_back = (back is not None and np.array_equal(back.numpy(), data)) if rank == 0 else back is None
+            ok_back = ok_back and all(k in tim for k in ("index", "scatter", "kernel", "checksum", "gather"))
+            # a corrupted content checksum: the reference's error on every rank
+            bad = ref.copy()
+            bad[-1] ^= 0x5A
+            try:
+                F.decompress_frame_sharded(torch.from_numpy(bad) if rank == 0 else None, True,
+                                           decoder=_OracleDecoder())
+                ok_back = False
+            except Exception as e:
+                ok_back = ok_back and "Content Checksum Error" in str(e)
+            # the host-staged content checksum alone == the oracle's XXH32 of the whole input
+            d = F.staged_checksum(mine)
+            ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
             res.append((ok, ok_back))
         q.put((rank, res))
         dist.barrier()
