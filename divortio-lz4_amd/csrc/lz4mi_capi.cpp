@@ -31,6 +31,8 @@ extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, c
                                               uint64_t*, uint64_t*, uint32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int32_t, int32_t, int32_t*, uint8_t*,
                                                   uint64_t, int32_t, int64_t*, hipStream_t);
+extern "C" hipError_t lz4mi_launch_compress_chain(const uint8_t*, uint64_t, int32_t, int32_t, int32_t, int32_t*,
+                                                  uint8_t*, const uint64_t*, uint32_t*, uint32_t, hipStream_t);
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
                                          uint32_t, int, uint8_t*, const uint64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_generate(uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
@@ -518,6 +520,57 @@ int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32
     // table entries written before it stay written
     if (ret[1]) return LZ4MI_ERR_RANGE;
     return ret[0];
+}
+
+int32_t lz4mi_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len, int32_t block_size,
+                             int32_t* table, uint8_t* out, const uint64_t* out_off, uint32_t* comp_len, uint32_t flags,
+                             void* stream) {
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
+    if (flags & LZ4MI_DEVICE_PTRS) return LZ4MI_ERR_ARG;   // host-only entry point (see header)
+    if (!src || !table || !out || !out_off || !comp_len || start < 0 || len < 0 || block_size <= 0 ||
+        (uint64_t)start + (uint64_t)len > src_total || block_size > (int32_t)LZ4MI_MAX_BLOCK)
+        return LZ4MI_ERR_ARG;
+    const uint32_t nb = (uint32_t)(((int64_t)len + block_size - 1) / block_size);
+    if (nb == 0) return LZ4MI_OK;
+    std::lock_guard<std::mutex> lk(g_ctx.mu);
+    hipStream_t s = g_ctx.stream;
+    (void)stream;
+    // the chain reaches at most 65535 bytes before `start`: stage src[base, start + len) and
+    // shift the table's positions by base (int32 wrap keeps the entries exact, as in
+    // lz4mi_compress_block_table)
+    const int64_t base = std::max<int64_t>(0, (int64_t)start - 65536);
+    const uint64_t sbytes = (uint64_t)start + len - base;
+    std::vector<uint64_t> d_off(nb);
+    uint64_t opos = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t n = std::min<uint64_t>(block_size, (uint64_t)len - (uint64_t)b * block_size);
+        d_off[b] = opos;
+        opos += round16(lz4mi_compress_bound(n));
+    }
+    LZ4MI_TRY(g_ctx.in.ensure(sbytes + 64, s));
+    LZ4MI_TRY(g_ctx.out.ensure(opos + 64, s));
+    LZ4MI_TRY(g_ctx.meta.ensure(16384 * 4 + (size_t)nb * 12 + 64, s));
+    std::vector<int32_t> t(16384);
+    for (int k = 0; k < 16384; ++k) t[k] = (int32_t)((uint32_t)table[k] - (uint32_t)base);
+    int32_t* d_table = g_ctx.meta.as<int32_t>();
+    uint64_t* m_off = (uint64_t*)(d_table + 16384);
+    uint32_t* m_len = (uint32_t*)(m_off + nb);
+    LZ4MI_TRY(hipMemcpyAsync(g_ctx.in.p, src + base, sbytes, hipMemcpyHostToDevice, s));
+    LZ4MI_TRY(hipMemcpyAsync(d_table, t.data(), 16384 * 4, hipMemcpyHostToDevice, s));
+    LZ4MI_TRY(hipMemcpyAsync(m_off, d_off.data(), 8ull * nb, hipMemcpyHostToDevice, s));
+    LZ4MI_TRY(lz4mi_launch_compress_chain(g_ctx.in.as<uint8_t>(), sbytes, (int32_t)(start - base), len, block_size,
+                                          d_table, g_ctx.out.as<uint8_t>(), m_off, m_len, nb, s));
+    LZ4MI_TRY(hipMemcpyAsync(comp_len, m_len, 4ull * nb, hipMemcpyDeviceToHost, s));
+    LZ4MI_TRY(hipMemcpyAsync(t.data(), d_table, 16384 * 4, hipMemcpyDeviceToHost, s));
+    LZ4MI_TRY(hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < nb; ++b)
+        if (comp_len[b])
+            LZ4MI_TRY(hipMemcpyAsync(out + out_off[b], g_ctx.out.as<uint8_t>() + d_off[b], comp_len[b],
+                                     hipMemcpyDeviceToHost, s));
+    LZ4MI_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < 16384; ++k) table[k] = (int32_t)((uint32_t)t[k] + (uint32_t)base);
+    return LZ4MI_OK;
 }
 
 int32_t lz4mi_xxh32_blocks(const uint8_t* in, const uint64_t* off, const uint32_t* len, uint32_t seed,

@@ -74,14 +74,61 @@ __device__ __forceinline__ uint32_t win_byte(uint32_t lo, uint32_t hi, uint32_t 
     return k < 64 ? __builtin_amdgcn_readlane(lo, k) : __builtin_amdgcn_readlane(hi, k - 64);
 }
 
+// ---- source ring of the dependent-block chain (lz4mi_compress_chain): the last
+// 64 KiB of the parse plus up to 32 KiB ahead of it, in LDS, so a probe's window,
+// the candidate's bytes and the literal copies are LDS reads instead of global
+// round trips (the chain is one wave's serial walk: its latency is the speed).
+// Byte p (absolute) lives at g_ring[p mod kRingBytes] while p in [lo, hi).
+constexpr uint32_t kRingBytes = 96 * 1024;
+constexpr int64_t kRingStep = 16 * 1024;     // refill granularity (16-byte aligned pieces)
+constexpr int64_t kRingAhead = 4096;         // refill when fewer bytes than this are ahead of the parse
+static_assert(kRingBytes - 65536 >= kRingStep + kRingAhead, "a refill never evicts a byte a probe can reach");
+__shared__ uint8_t g_ring[kRingBytes];
+
+struct Ring {
+    int64_t lo, hi;
+};
+
+template <bool RING>
+__device__ __forceinline__ uint32_t sbyte(const CompJob& j, const Ring& r, int64_t p) {
+    if (RING && p >= r.lo && p < r.hi) return g_ring[(uint32_t)p % kRingBytes];
+    return src_byte(j, p);
+}
+
+// Bring at least kRingAhead bytes ahead of position i into the ring (whole wave).
+__device__ void ring_advance(const CompJob& j, Ring& r, int lane, int64_t i) {
+    while ((uint64_t)r.hi < j.src_total && r.hi - i < kRingAhead + 256) {
+        const int64_t n = (int64_t)j.src_total - r.hi < kRingStep ? (int64_t)j.src_total - r.hi : kRingStep;
+        for (int64_t k = 16 * lane; k < n; k += 16 * kWave) {
+            const int64_t p = r.hi + k;
+            const uint32_t q = (uint32_t)p % kRingBytes;
+            if (k + 16 <= n) {
+                uint4 v;
+                __builtin_memcpy(&v, j.src + p, 16);
+                *(uint4*)&g_ring[q] = v;
+            } else {
+                for (int64_t t = 0; k + t < n; ++t) g_ring[q + t] = j.src[p + t];
+            }
+        }
+        __syncthreads();
+        r.hi += n;
+        if (r.hi - r.lo > (int64_t)kRingBytes) r.lo = r.hi - kRingBytes;
+    }
+}
+
 // dst[p, p+n) = v (wave-parallel).
 __device__ void wave_fill(const CompJob& j, int lane, int64_t p, int64_t n, uint32_t v) {
     for (int64_t k = lane; k < n; k += kWave) put_byte(j, p + k, v);
 }
 
 // dst[d, d+n) = src[s, s+n) (wave-parallel, aligned dword stores where possible).
-__device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int64_t n) {
+template <bool RING = false>
+__device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int64_t n, const Ring* rg = nullptr) {
     if (n <= 0) return;
+    if (RING && s >= rg->lo && s + n <= rg->hi) {     // literals in the ring: LDS reads, byte stores in order
+        for (int64_t k = lane; k < n; k += kWave) put_byte(j, d + k, g_ring[(uint32_t)(s + k) % kRingBytes]);
+        return;
+    }
     uintptr_t da = (uintptr_t)(j.dst + d);
     int64_t head = (int64_t)((4 - (da & 3)) & 3);
     if (head > n) head = n;
@@ -176,8 +223,9 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
 // A run of more than 64 literals is one output.set() in the reference (blockCompress.js:100,
 // :198), which throws a RangeError instead of writing when the run does not fit: `range`
 // is set and the position after the length bytes returned (what was written stays).
+template <bool RING = false>
 __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t anchor, int64_t lit,
-                                 uint32_t mnib, bool& range) {
+                                 uint32_t mnib, bool& range, const Ring* rg = nullptr) {
     uint32_t tok = (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib;
     const int64_t tok_pos = op;
     if (lane == 0) put_byte(j, op, tok);
@@ -195,26 +243,38 @@ __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t
         range = true;
         return op;
     }
-    wave_copy(j, lane, op, anchor, lit);
+    wave_copy<RING>(j, lane, op, anchor, lit, rg);
     return op + lit;
 }
 
-__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range) {
+// A register whose load has been waited for: redefine it opaquely so the compiler's
+// wait insertion stops tracking it. Without this, the window bytes carried into the
+// next probe are waited for with vmcnt(0), which also waits for every store the
+// previous sequence's emission issued after them: a store round trip per sequence on
+// the chain (the loads themselves completed long before).
+__device__ __forceinline__ void settle32(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
+template <bool RING = false>
+__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range, Ring* rg = nullptr) {
     const int64_t end = (int64_t)j.start + j.len;
     const int64_t mflimit = end - 12;
     const int64_t matchlimit = end - 5;
     int64_t i = j.start, anchor = j.start, op = j.dst_pos;
     uint32_t miss = 67;
     // 128-byte source window [wi, wi+128): lane k holds bytes wi+k and wi+64+k
+    if (RING) ring_advance(j, *rg, lane, i);
     int64_t wi = i;
-    uint32_t wlo = src_byte(j, wi + lane), whi = src_byte(j, wi + 64 + lane);
+    uint32_t wlo = sbyte<RING>(j, *rg, wi + lane), whi = sbyte<RING>(j, *rg, wi + 64 + lane);
 
     while (i < mflimit) {
+        if (RING && rg->hi - i < kRingAhead) ring_advance(j, *rg, lane, i);
         if (i + 4 > wi + 128) {
             wi = i;
-            wlo = src_byte(j, wi + lane);
-            whi = src_byte(j, wi + 64 + lane);
+            wlo = sbyte<RING>(j, *rg, wi + lane);
+            whi = sbyte<RING>(j, *rg, wi + 64 + lane);
         }
+        settle32(wlo);
+        settle32(whi);
         uint32_t k0 = (uint32_t)(i - wi);
         uint32_t seq = win_byte(wlo, whi, k0) | (win_byte(wlo, whi, k0 + 1) << 8) |
                        (win_byte(wlo, whi, k0 + 2) << 16) | (win_byte(wlo, whi, k0 + 3) << 24);
@@ -229,10 +289,11 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         }
         // fetch the candidate's 128 bytes and re-anchor the window at i, one round trip
         wi = i;
-        wlo = src_byte(j, i + lane);
-        whi = src_byte(j, i + 64 + lane);
-        uint32_t clo = src_byte(j, (int64_t)cand + lane), chi = src_byte(j, (int64_t)cand + 64 + lane);
+        wlo = sbyte<RING>(j, *rg, i + lane);
+        whi = sbyte<RING>(j, *rg, i + 64 + lane);
+        uint32_t clo = sbyte<RING>(j, *rg, (int64_t)cand + lane), chi = sbyte<RING>(j, *rg, (int64_t)cand + 64 + lane);
         uint64_t neq_lo = __ballot(wlo != clo);
+        settle32(wlo);
         if (neq_lo & 0xFull) {                    // the 4-byte content check failed
             i += miss++ >> 6;
             continue;
@@ -241,6 +302,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         // forward extension: e = i+4.. while e < matchlimit and bytes equal
         int64_t lim = matchlimit - i;             // compare bytes k in [4, lim)
         uint64_t neq_hi = __ballot(whi != chi);
+        settle32(whi);
         int64_t e;
         {
             uint64_t m_lo = neq_lo & ~0xFull;
@@ -256,8 +318,8 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
                         e = p + match_extent(j, lane, p, mp, matchlimit - p);
                         break;
                     }
-                    uint32_t a0 = src_byte(j, p + lane), a1 = src_byte(j, p + 64 + lane);
-                    uint32_t b0 = src_byte(j, mp + lane), b1 = src_byte(j, mp + 64 + lane);
+                    uint32_t a0 = sbyte<RING>(j, *rg, p + lane), a1 = sbyte<RING>(j, *rg, p + 64 + lane);
+                    uint32_t b0 = sbyte<RING>(j, *rg, mp + lane), b1 = sbyte<RING>(j, *rg, mp + 64 + lane);
                     uint64_t n0 = __ballot(a0 != b0), n1 = __ballot(a1 != b1);
                     int64_t g = n0 ? __builtin_ctzll(n0) : (n1 ? 64 + __builtin_ctzll(n1) : 128);
                     int64_t l2 = matchlimit - p;
@@ -269,7 +331,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         }
         int64_t mcode = e - i - 4;
         int64_t lit = i - anchor;
-        op = emit_literals(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range);
+        op = emit_literals<RING>(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range, rg);
         if (range) return op - j.dst_pos;
         uint32_t off = (uint32_t)(i - cand);
         if (lane == 0) { put_byte(j, op, off & 255); put_byte(j, op + 1, (off >> 8) & 255); }
@@ -284,7 +346,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         i = e;
         anchor = e;
     }
-    op = emit_literals(j, lane, op, anchor, end - anchor, 0, range);
+    op = emit_literals<RING>(j, lane, op, anchor, end - anchor, 0, range, rg);
     return op - j.dst_pos;
 }
 
@@ -308,7 +370,8 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
     for (int k = lane; k < 16384; k += kWave) T[k] = j.table ? j.table[k] : 0;
     __syncthreads();
     bool range = false;
-    int64_t n = compress_block_wave(j, T, lane, range);
+    Ring none{0, 0};
+    int64_t n = compress_block_wave<false>(j, T, lane, range, &none);
     __syncthreads();
     if (j.table)
         for (int k = lane; k < 16384; k += kWave) j.table[k] = T[k];
@@ -676,10 +739,39 @@ __global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
 // stores complete before the next table access). Table reads are plain loads:
 // the CU's L1 sees the wave's own completed stores (nontemporal loads and an
 // atomic exchange at the head, used until round 2, cost 7 %: 208.8 vs 194.5 ms).
+#ifndef LZ4MI_GT16
+#define LZ4MI_GT16 0   // 1: the batch encoder's tables as 15-bit positions in global + 2-bit epoch codes in LDS
+#endif
+
 struct GtShared {
     uint8_t ring[kRing];
     uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
+#if LZ4MI_GT16
+    uint32_t code[kCodeWords];   // 2-bit epoch code per table entry (as FastShared's)
+#endif
 };
+
+#if LZ4MI_GT16
+// A 15-bit table entry + its epoch code -> the position it stands for (-1: empty/stale),
+// exactly as compress_block_fast decodes its LDS table.
+__device__ __forceinline__ int32_t gt16_decode(uint32_t lo, uint32_t cd, int32_t g) {
+    if (cd == (uint32_t)((g + 1) & 3)) return -1;
+    const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
+    return ge < 0 ? -1 : ((ge << 15) | (int32_t)(lo & 0x7FFFu));
+}
+__device__ __forceinline__ uint32_t gt_code_of(const GtShared& F, uint32_t h) {
+    return (F.code[h >> 4] >> ((h & 15) * 2)) & 3u;
+}
+__device__ void gt_scrub_epoch(GtShared& F, int lane, int32_t g) {
+    const uint32_t X = (uint32_t)(g & 3) * 0x55555555u, Y = (uint32_t)((g + 1) & 3) * 0x55555555u;
+    for (int w = lane; w < kCodeWords; w += kWave) {
+        const uint32_t v = F.code[w], x = v ^ X;
+        const uint32_t eq = ~(x | (x >> 1)) & 0x55555555u;
+        const uint32_t fm = eq | (eq << 1);
+        F.code[w] = (v & ~fm) | (Y & fm);
+    }
+}
+#endif
 
 __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, int lane) {
     const int32_t n = j.len;
@@ -692,9 +784,19 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
     bool pv = false;             // the previous match, emitted while the next probe's loads are in flight
     int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
     uint32_t p_off = 0;
+#if LZ4MI_GT16
+    uint16_t* T16 = (uint16_t*)T;   // 32 KiB of the block's 64 KiB slot
+    int32_t g = 0;                  // epoch of the parse position (32 KiB each)
+    for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
+    for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
+#else
     for (int k = lane; k < 16384 / 4; k += kWave) ((uint4*)T)[k] = make_uint4(0, 0, 0, 0);
+#endif
     wait_vmem();                 // the table is zero before the first exchange
     while (i < mflimit) {
+#if LZ4MI_GT16
+        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+#endif
         // ---- the probe at i: one exchange, then verification + speculative extension windows
         // high wave priority on the chain (probe, hit test, extension); the previous
         // sequence's emission below, off the chain, runs at low priority while its loads
@@ -710,6 +812,17 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
             seq0 = uniform(ld_u32(j, i));
         }
         const uint32_t h0 = (seq0 * kP1) >> 18;
+#if LZ4MI_GT16
+        int32_t cand0 = -1;
+        if (lane == 0) {   // read and replace: 15-bit position in global, epoch code in LDS
+            cand0 = gt16_decode(T16[h0], gt_code_of(F, h0), g);
+            T16[h0] = (uint16_t)(i & 0x7FFF);
+            const uint32_t sh = (h0 & 15) * 2;
+            F.code[h0 >> 4] = (F.code[h0 >> 4] & ~(3u << sh)) | ((uint32_t)(g & 3) << sh);
+        }
+        cand0 = (int32_t)uniform((uint32_t)cand0);
+        if (cand0 < 0 || i - cand0 < 1 || i - cand0 > 65535) cand0 = -1;
+#else
         int32_t old = 0;
         if (lane == 0) {   // read and replace (one wave owns the table: no atomic needed)
             old = T[h0];
@@ -718,6 +831,7 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         old = (int32_t)uniform((uint32_t)old);
         int32_t cand0 = old - 1;
         if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
+#endif
         uint32_t aw = 0, bw = 0;
         bool hit0 = false;
         if (cand0 >= 0) {
@@ -769,7 +883,12 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         if (i >= mflimit) break;
         const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
         const uint32_t step = (c + lane) >> 6;
+#if LZ4MI_GT16
+        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+        bool act = p < mflimit && (p >> 15) == g;   // probes of the next epoch: the next batch
+#else
         bool act = p < mflimit;
+#endif
         uint32_t seq = 0;
         {
             const int32_t off = p - wb;
@@ -797,15 +916,31 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         }
         const int nb = __popcll(__ballot(act));
         int32_t cand = -1;
+#if LZ4MI_GT16
+        if (act) {
+            cand = gt16_decode(T16[h], gt_code_of(F, h), g);
+            if (cand < 0 || p - cand < 1 || p - cand > 65535) cand = -1;
+        }
+#else
         if (act) {
             const int32_t ov = T[h];
             cand = ov - 1;
             if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
         }
+#endif
         const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
         const uint64_t hm = __ballot(cand >= 0 && vw == seq);
         const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+#if LZ4MI_GT16
+        if (lane < nprobe) {                                   // the probes that happen insert their position
+            T16[h] = (uint16_t)(p & 0x7FFF);
+            const uint32_t sh = (h & 15) * 2;                  // distinct hashes, maybe one code word: LDS atomics
+            atomicAnd(&F.code[h >> 4], ~(3u << sh));
+            atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
+        }
+#else
         if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
+#endif
         wait_vmem();                                           // ... before the next table access
         if (!hm) {
             i = lane_val(p + (int32_t)step, nb - 1);
@@ -848,6 +983,43 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, in
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
+// Dependent blocks (the reference's LZ4.compress default, bufferCompress.js:182-236): the
+// blocks of one frame in order, one hash table carried from block to block (the caller's,
+// in and out), every block's output in its own slot. One wave walks the whole chain; the
+// table (64 KiB) and the source ring (96 KiB) fill the CU's LDS.
+struct ChainArgs {
+    const uint8_t* src;
+    uint64_t src_total;
+    int32_t start, len, bsize;
+    int32_t* table;
+    uint8_t* out;
+    const uint64_t* out_off;
+    uint32_t* comp_len;
+    uint32_t nblocks;
+};
+
+__global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
+    __shared__ int32_t T[16384];
+    const int lane = threadIdx.x;
+    for (int k = lane; k < 16384; k += kWave) T[k] = a.table[k];
+    __syncthreads();
+    int64_t lo = (int64_t)a.start - 65536;
+    lo = lo < 0 ? 0 : (lo & ~(int64_t)15);
+    Ring r{lo, lo};
+    for (uint32_t b = 0; b < a.nblocks; ++b) {
+        const int64_t s0 = (int64_t)a.start + (int64_t)b * a.bsize;
+        const int64_t rest = (int64_t)a.start + a.len - s0;
+        const int32_t n = (int32_t)(rest < a.bsize ? rest : a.bsize);
+        CompJob j{a.src, a.src_total, (int32_t)s0, n, a.out + a.out_off[b],
+                  (uint64_t)n + (uint64_t)n / 255u + 16u, 0, nullptr};
+        bool range = false;
+        const int64_t w = compress_block_wave<true>(j, T, lane, range, &r);
+        if (lane == 0) a.comp_len[b] = (uint32_t)w;
+    }
+    __syncthreads();
+    for (int k = lane; k < 16384; k += kWave) a.table[k] = T[k];
+}
+
 }  // namespace lz4mi
 
 #if LZ4MI_CPROFILE
@@ -884,5 +1056,14 @@ extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t* src, uint64_t s
     a.single = lz4mi::CompJob{src, src_total, start, len, dst, dst_total, dst_pos, table};
     a.single_ret = ret;
     hipLaunchKernelGGL(lz4mi::lz4mi_compress_kernel, dim3(1), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t lz4mi_launch_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len,
+                                                  int32_t bsize, int32_t* table, uint8_t* out, const uint64_t* out_off,
+                                                  uint32_t* comp_len, uint32_t nblocks, hipStream_t stream) {
+    if (nblocks == 0) return hipSuccess;
+    lz4mi::ChainArgs a{src, src_total, start, len, bsize, table, out, out_off, comp_len, nblocks};
+    hipLaunchKernelGGL(lz4mi::lz4mi_compress_chain_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }

@@ -47,9 +47,6 @@
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
 #endif
-#ifndef LZ4MI_PIECES
-#define LZ4MI_PIECES 0     // 0: every table through the general (one match per lane) output (A/B switch)
-#endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
@@ -97,7 +94,6 @@ constexpr int kPeriodBulk = 1024;             // longer periodic runs are genera
 constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
 
 struct DecShared {
-    uint32_t stage_pad[4];        // piece output: literal windows start up to 15 bytes before a run
     uint32_t stage[kStageWords];
     union {
         struct {
@@ -115,10 +111,9 @@ struct DecShared {
         uint16_t nxt[kLim];       // parse: next-token table
         uint32_t pme[kLim / 2];   // output: ends of the pending matches
     };
-    alignas(8) uint32_t pms[kMaxSeq];   // output: starts of the pending matches (piece output: done bitmap)
+    uint32_t pms[kMaxSeq];        // output: starts of the pending matches
 };
 static_assert(kLim / 2 >= kMaxSeq, "pending list must fit in the next-token table");
-static_assert(offsetof(DecShared, stage) == 16, "the stage follows its 16-byte front pad");
 
 // LDS a whole-wave periodic run may copy its pattern into, by phase of the
 // chunk: round 1 (the pending list is not built yet), rounds 2+ (the staged
@@ -131,7 +126,7 @@ struct PatBuf {
 __device__ __forceinline__ PatBuf no_pat() { return PatBuf{nullptr, 0}; }   // literal runs
 __device__ __forceinline__ PatBuf pat_round1(DecShared& S) { return PatBuf{S.pms, (int32_t)sizeof(S.pms)}; }
 __device__ __forceinline__ PatBuf pat_rounds(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(S.stage)}; }
-__device__ __forceinline__ PatBuf pat_all(DecShared& S) { return PatBuf{S.stage_pad, (int32_t)sizeof(DecShared)}; }
+__device__ __forceinline__ PatBuf pat_all(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(DecShared)}; }
 __device__ __forceinline__ PatBuf pat_cut(DecShared& S) {
     return PatBuf{S.pme, (int32_t)(sizeof(DecShared) - offsetof(DecShared, pme))};
 }
@@ -439,14 +434,34 @@ __device__ __forceinline__ uint4 load16(const Ctx& c, const DecShared& S, int32_
     return v;
 }
 
+// A lane's 16 bytes of a sink for the pipelines' empty slots. With the copy pipelines'
+// loads and stores under `if`, a branch may skip them, the compiler cannot count the
+// wave's outstanding vector-memory ops, and every use of a loaded value waited with
+// vmcnt(0) — for all loads and stores in flight, including the next stage's loads the
+// pipeline had just issued. Unconditional loads and stores (an empty slot reads and
+// writes here) keep the counts static: a store waits only for its own stage's loads.
+__device__ uint4 g_dec_sink[kWave];
+__device__ __forceinline__ uint8_t* sink16() { return (uint8_t*)&g_dec_sink[threadIdx.x]; }
+
 template <uint32_t KIND, bool TWO, int NB>
 __device__ __forceinline__ void load_slots(const Ctx& c, const DecShared& S, const Slot (&s)[NB], uint4 (&A)[NB],
                                            uint4 (&B)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         if (LZ4MI_ABLATE == 5) { A[j] = make_uint4(0, 0, 0, 0); B[j] = A[j]; continue; }
-        if (s[j].wm >> 8) A[j] = load16<KIND>(c, S, s[j].a);
-        if (TWO && (s[j].wm >> 8) == 2) B[j] = load16<KIND>(c, S, s[j].a - s[j].per);
+        if (KIND == R_LDS) {
+            if (s[j].wm >> 8) A[j] = load16<KIND>(c, S, s[j].a);
+        } else {
+            const uint8_t* base = KIND == R_COMP ? c.blk : c.dst;
+            const uint8_t* pa = (s[j].wm >> 8) ? base + s[j].a : sink16();
+            const u32x4_t t = *(const u32x4_t*)pa;
+            A[j] = make_uint4(t.x, t.y, t.z, t.w);
+            if (TWO) {
+                const uint8_t* pb = (s[j].wm >> 8) == 2 ? base + s[j].a - s[j].per : sink16();
+                const u32x4_t u = *(const u32x4_t*)pb;
+                B[j] = make_uint4(u.x, u.y, u.z, u.w);
+            }
+        }
     }
 }
 
@@ -455,18 +470,16 @@ __device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Sl
                                             const uint4 (&B)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+        // pipe() takes runs of >= 16 bytes only (wave runs): every piece is 16 bytes wide
         const uint32_t mode = s[j].wm >> 8;
-        if (!mode) continue;
         uint4 v = A[j];
         if (TWO && mode == 2) v = pick4(A[j], B[j], s[j].k);
         else if (mode == 3) v = expand_period(A[j], s[j].k, s[j].per);
         if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
-            if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pms[0] = 1;
+            if (mode && (v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
-        const uint32_t w = s[j].wm & 255u;
-        if (w == 16) out16(c.dst + s[j].y, v);
-        else store_w(c.dst + s[j].y, v, w);
+        out16(mode ? c.dst + s[j].y : sink16(), v);
     }
 }
 
@@ -583,14 +596,16 @@ struct LaneMatchGen {
     }
 };
 
+// Every slot loads and stores, an empty one from / to this lane's 16 bytes of a sink
+// (g_dec_sink): with no branch around them the compiler can count the wave's outstanding
+// vector-memory ops and wait only for the stage a store needs.
 template <int NB>
 __device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], uint4 (&A)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        if (s[j].w) {
-            const u32x4_t t = *(const u32x4_t*)(c.dst + s[j].a);
-            A[j] = make_uint4(t.x, t.y, t.z, t.w);
-        }
+        const uint8_t* p = s[j].w ? c.dst + s[j].a : sink16();
+        const u32x4_t t = *(const u32x4_t*)p;
+        A[j] = make_uint4(t.x, t.y, t.z, t.w);
     }
 }
 
@@ -598,12 +613,12 @@ template <int NB>
 __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        if (!s[j].w) continue;
         if (LZ4MI_ABLATE == 4) {
-            if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;
+            if (s[j].w && (A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
-        out16(c.dst + s[j].y, A[j]);
+        uint8_t* p = s[j].w ? c.dst + s[j].y : sink16();
+        out16(p, A[j]);
     }
 }
 
@@ -719,9 +734,26 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
     }
 }
 
+// A run shorter than 16 bytes (only the cut sequence's runs reach wave_run that short):
+// lane t copies byte t; every source byte is final (non-periodic: the source ends at or
+// before y; periodic: [src, src + period) lies before y).
+__device__ __forceinline__ void small_run(const Ctx& c, const DecShared& S, int lane, const Run& R) {
+    if (lane >= R.n) return;
+    const int32_t t = R.period ? lane % R.period : lane;
+    uint32_t v;
+    if (R.kind == R_LDS) v = ((const uint8_t*)S.stage)[R.src + lane];
+    else if (R.kind == R_COMP) v = c.blk[R.src + lane];
+    else v = hist_byte(c, (int64_t)R.src + t);
+    c.dst[R.y + lane] = (uint8_t)v;
+}
+
 // The whole wave writes one run (uniform R).
 __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R, PatBuf B) {
     if (R.kind == R_NONE || R.n <= 0) return;
+    if (R.n < 16) {          // pipe() writes whole 16-byte pieces
+        small_run(c, S, lane, R);
+        return;
+    }
     // (a byte-wise periodic run whose source is inside the buffer qualifies too:
     // periodic_run reads only [src, src + period))
     const bool in_buf = R.kind == R_HIST || (R.kind == R_BYTES && c.out_off + R.src >= 0);
@@ -759,8 +791,8 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         const uint4 v0 = stage16(S.stage, L.src + d0);
         const uint4 v1 = stage16(S.stage, L.src + d1);
         if (LZ4MI_ABLATE == 4) continue;
-        if (q < np) out16(c.dst + L.y + d0, v0);
-        if (q + 1 < np) out16(c.dst + L.y + d1, v1);
+        out16(q < np ? c.dst + L.y + d0 : sink16(), v0);
+        out16(q + 1 < np ? c.dst + L.y + d1 : sink16(), v1);
     }
     if (__ballot(n > 0 && n < 16)) {                       // shorter runs: two overlapping 8/4/2/1-byte stores
         if (n > 0 && n < 16) {
@@ -889,251 +921,6 @@ __device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t ns
             wait_vmem();
         }
     }
-}
-
-// ------------------------------------------------------------ piece output
-// Output of a table whose matches are all plain (length >= 16, offset >= length,
-// source >= 16 bytes into the buffer) and whose output fits kLim pieces: the
-// chunk's output [O, Ecap) is cut into 16-byte pieces on the absolute 16-byte
-// grid and lane l assembles pieces 64 i + l, so each store instruction writes
-// one aligned 1 KiB row (one match per lane wrote 16-byte pieces ~64 bytes
-// apart: a fifth of the store path's width). A piece holds at most two match
-// segments (a match is >= 16 bytes) plus literal bytes: literal bytes come from
-// the stage (LDS), each match segment from one 16-byte window of earlier output,
-// loaded after the piece is planned (all windows of a batch of rows in flight
-// together). A match whose source is this table's output is first mapped back
-// through the sequences that wrote it (to finished output or to the stage);
-// what cannot be mapped waits for the rounds: a piece is taken once every piece
-// its windows read is stored (done bitmap, one ballot per row). The earliest
-// pending piece is always ready (its sources lie in earlier pieces), so the
-// rounds end.
-constexpr uint32_t kSrcGlobal = 0u, kSrcLds = 1u, kSrcPend = 2u;
-constexpr int kPieceRows = (kLim + kWave - 1) / kWave;   // rows of 64 pieces a table may have
-constexpr int kPB = 6;                                   // rows planned and loaded together
-static_assert(kPieceRows <= 32, "pending rows fit one 32-bit mask");
-static_assert(sizeof(uint64_t) * kPieceRows <= sizeof(uint32_t) * kMaxSeq, "done bitmap fits the pending list");
-
-__device__ __forceinline__ uint32_t enc_src(uint32_t kind, int32_t v) { return (kind << 28) | ((uint32_t)v & 0x0FFFFFFFu); }
-__device__ __forceinline__ int32_t src_val(uint32_t e) { return ((int32_t)(e << 4)) >> 4; }
-
-// 16 staged bytes from stage index idx (>= -16: the front pad).
-__device__ __forceinline__ uint4 lit16(const DecShared& S, int32_t idx) { return stage16(S.stage_pad, idx + 16); }
-
-__device__ __forceinline__ uint64_t lowmask64(int32_t n) {
-    return n >= 8 ? ~0ull : (n <= 0 ? 0ull : ((1ull << (8 * n)) - 1ull));
-}
-// bytes [a, b) of W over v
-__device__ __forceinline__ uint4 overlay(uint4 v, uint4 W, int32_t a, int32_t b) {
-    const uint64_t ml = lowmask64(b) & ~lowmask64(a), mh = lowmask64(b - 8) & ~lowmask64(a - 8);
-    const uint64_t vl = ((uint64_t)v.y << 32) | v.x, vh = ((uint64_t)v.w << 32) | v.z;
-    const uint64_t wl = ((uint64_t)W.y << 32) | W.x, wh = ((uint64_t)W.w << 32) | W.z;
-    const uint64_t rl = (vl & ~ml) | (wl & ml), rh = (vh & ~mh) | (wh & mh);
-    return make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
-}
-
-// bytes [a, b) of v (1 <= b - a <= 15) to p + a
-__device__ __forceinline__ void store_range(uint8_t* p, uint4 v, int32_t a, int32_t b) {
-    unsigned __int128 x;
-    __builtin_memcpy(&x, &v, 16);
-    x >>= 8 * a;
-    const int32_t n = b - a;
-    uint8_t* q = p + a;
-    if (n & 8) { const uint64_t t = (uint64_t)x; __builtin_memcpy(q, &t, 8); x >>= 64; q += 8; }
-    if (n & 4) { const uint32_t t = (uint32_t)x; __builtin_memcpy(q, &t, 4); x >>= 32; q += 4; }
-    if (n & 2) { const uint16_t t = (uint16_t)x; __builtin_memcpy(q, &t, 2); x >>= 16; q += 2; }
-    if (n & 1) *q = (uint8_t)x;
-}
-
-struct PieceGrid {
-    int32_t O, E, Ecap, Pbase;   // table output [O, E), written [O, Ecap), piece j at Pbase + 16 j
-    uint32_t np, nseq;
-};
-
-// Last sequence starting at or before rs (rs in [O, Ecap)), from the piece map.
-__device__ __forceinline__ uint32_t seq_at(const DecShared& S, const PieceGrid& G, int32_t rs) {
-    uint32_t k = S.nxt[(uint32_t)(rs - G.Pbase) >> 4];
-    while (k + 1 < G.nseq && (int32_t)S.t_out[k + 1] <= rs) ++k;
-    return k;
-}
-
-// [rs, re) of this table's output mapped back through the sequences that wrote
-// it: kSrcGlobal (rs is now finished output before O), kSrcLds (rs = stage index
-// of its first byte) or kSrcPend.
-__device__ uint32_t remap_range(const DecShared& S, const PieceGrid& G, int32_t& rs, int32_t re) {
-    for (int d = 0; d < 8; ++d) {
-        if (re <= G.O) return kSrcGlobal;
-        if (rs < G.O) return kSrcPend;
-        const uint32_t k = seq_at(S, G, rs);
-        const int32_t t0 = (int32_t)S.t_out[k];
-        const SeqInfo q = seq_info(S, k);
-        const int32_t ms = t0 + q.ll;
-        if (re <= ms) {
-            rs = q.lit + (rs - t0);
-            return kSrcLds;
-        }
-        const int32_t te = k + 1 < G.nseq ? (int32_t)S.t_out[k + 1] : G.E;
-        if (rs < ms || re > te) return kSrcPend;
-        rs -= q.off;
-        re -= q.off;
-    }
-    return kSrcPend;
-}
-
-__device__ __forceinline__ bool piece_done(const DecShared& S, uint32_t j) {
-    const uint64_t* done = (const uint64_t*)S.pms;
-    return ((done[j >> 6] >> (j & 63)) & 1ull) != 0;
-}
-
-// Every byte of [rs, re) (re - rs <= 16) is finished output: before O, or in stored pieces.
-__device__ __forceinline__ bool src_ready(const DecShared& S, const PieceGrid& G, int32_t rs, int32_t re) {
-    if (re <= G.O) return true;
-    const int32_t s0 = rs > G.O ? rs : G.O;
-    return piece_done(S, (uint32_t)(s0 - G.Pbase) >> 4) && piece_done(S, (uint32_t)(re - 1 - G.Pbase) >> 4);
-}
-
-// Plan piece j: literal bytes into v, up to two match windows (block-relative window
-// starts a0/a1, byte ranges r0/r1 = lo | hi << 8, 0 = none). Returns false when a
-// window's source is not finished yet.
-__device__ __forceinline__ bool plan_out_piece(const DecShared& S, const PieceGrid& G, uint32_t j, uint4& v,
-                                               int32_t& a0, uint32_t& r0, int32_t& a1, uint32_t& r1) {
-    const int32_t P = G.Pbase + 16 * (int32_t)j;
-    const int32_t hi = P + 16 < G.Ecap ? P + 16 : G.Ecap;
-    int32_t x = P > G.O ? P : G.O;
-    uint32_t k = S.nxt[j];
-    bool ready = true;
-    v = make_uint4(0, 0, 0, 0);
-    a0 = a1 = 0;
-    r0 = r1 = 0;
-    while (x < hi) {
-        const int32_t t0 = (int32_t)S.t_out[k];
-        const SeqInfo q = seq_info(S, k);
-        const int32_t ms = t0 + q.ll;
-        const int32_t t1 = k + 1 < G.nseq ? (int32_t)S.t_out[k + 1] : G.E;
-        int32_t e;
-        if (x < ms) {                                       // literal bytes
-            e = ms < hi ? ms : hi;
-            v = overlay(v, lit16(S, q.lit - t0 + P), x - P, e - P);
-        } else {                                            // match bytes
-            e = t1 < hi ? t1 : hi;
-            const uint32_t r = S.t_rsrc[k];
-            const int32_t val = src_val(r);
-            if ((r >> 28) == kSrcLds) {
-                v = overlay(v, lit16(S, val - ms + P), x - P, e - P);
-            } else {
-                int32_t wa;
-                if ((r >> 28) == kSrcGlobal) {
-                    wa = val - ms + P;
-                } else {
-                    wa = P - q.off;
-                    ready = ready && src_ready(S, G, x - q.off, e - q.off);
-                }
-                const uint32_t rr = (uint32_t)(x - P) | ((uint32_t)(e - P) << 8);
-                if (r0 == 0) { a0 = wa; r0 = rr; }
-                else { a1 = wa; r1 = rr; }
-            }
-        }
-        x = e;
-        if (x >= t1) ++k;
-    }
-    return ready;
-}
-
-// Returns false if a round stores nothing while pieces are pending (cannot happen for
-// a table that qualifies; the caller then writes the table the general way).
-__device__ __attribute__((noinline)) bool piece_output(const Ctx& c, DecShared& S, int lane, uint32_t nseq, int64_t total) {
-    PieceGrid G;
-    G.O = (int32_t)c.O;
-    G.E = (int32_t)(c.O + total);
-    G.Ecap = G.E < c.cap ? G.E : c.cap;
-    const int32_t dmod = (int32_t)((uintptr_t)c.dst & 15u);
-    G.Pbase = G.O - ((G.O + dmod) & 15);
-    G.np = G.Ecap > G.O ? (uint32_t)(G.Ecap - G.Pbase + 15) >> 4 : 0u;
-    G.nseq = nseq;
-    if (G.np == 0) return true;
-    const uint32_t nrows = (G.np + kWave - 1) / kWave;
-    // piece -> sequence holding its first byte (piece 0 holds O, the first sequence's start)
-    if (lane == 0) S.nxt[0] = 0;
-    for (uint32_t k = lane; k < nseq; k += kWave) {
-        const int32_t t0 = (int32_t)S.t_out[k];
-        const int32_t t1 = k + 1 < nseq ? (int32_t)S.t_out[k + 1] : G.E;
-        const uint32_t j0 = (uint32_t)(t0 - G.Pbase + 15) >> 4;
-        uint32_t j1 = (uint32_t)(t1 - G.Pbase + 15) >> 4;
-        if (j1 > G.np) j1 = G.np;
-        for (uint32_t j = j0; j < j1; ++j) S.nxt[j] = (uint16_t)k;
-    }
-    __syncthreads();
-    // each match's source mapped back through this table once (kSrcPend: per piece, by rounds)
-    for (uint32_t k = lane; k < nseq; k += kWave) {
-        const int32_t t0 = (int32_t)S.t_out[k];
-        const SeqInfo q = seq_info(S, k);
-        const int32_t ms = t0 + q.ll;
-        uint32_t r = enc_src(kSrcGlobal, 0);
-        if (q.ml && ms < G.Ecap) {
-            int32_t rs = ms - q.off;
-            const int32_t re = rs + (q.ml < G.Ecap - ms ? q.ml : G.Ecap - ms);
-            const uint32_t kind = remap_range(S, G, rs, re);
-            r = enc_src(kind, kind == kSrcPend ? ms - q.off : rs);
-        }
-        S.t_rsrc[k] = r;
-    }
-    if (lane < kPieceRows) ((uint64_t*)S.pms)[lane] = 0ull;
-    __syncthreads();
-    uint32_t pend = nrows >= 32 ? ~0u : ((1u << nrows) - 1u);
-    while (__ballot(pend != 0)) {
-        uint32_t stored = 0;
-        for (uint32_t i0 = 0; i0 < nrows; i0 += kPB) {
-            const uint32_t bm = (pend >> i0) & ((1u << kPB) - 1u);
-            if (!__ballot(bm != 0)) continue;
-            uint4 V[kPB], A0[kPB], A1[kPB];
-            int32_t a0[kPB], a1[kPB];
-            uint32_t r0[kPB], r1[kPB];
-            bool go[kPB];
-#pragma unroll
-            for (int b = 0; b < kPB; ++b) {
-                const uint32_t j = (i0 + b) * kWave + lane;
-                go[b] = false;
-                if (((bm >> b) & 1u) && j < G.np) go[b] = plan_out_piece(S, G, j, V[b], a0[b], r0[b], a1[b], r1[b]);
-                else if (((bm >> b) & 1u)) pend &= ~(1u << (i0 + b));     // past the end: nothing to write
-            }
-#pragma unroll
-            for (int b = 0; b < kPB; ++b) {
-                if (go[b] && r0[b]) {
-                    const u32x4_t t = *(const u32x4_t*)(c.dst + a0[b]);
-                    A0[b] = make_uint4(t.x, t.y, t.z, t.w);
-                }
-                if (go[b] && r1[b]) {
-                    const u32x4_t t = *(const u32x4_t*)(c.dst + a1[b]);
-                    A1[b] = make_uint4(t.x, t.y, t.z, t.w);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < kPB; ++b) {
-                if (!go[b]) continue;
-                uint4 v = V[b];
-                if (r0[b]) v = overlay(v, A0[b], (int32_t)(r0[b] & 255u), (int32_t)(r0[b] >> 8));
-                if (r1[b]) v = overlay(v, A1[b], (int32_t)(r1[b] & 255u), (int32_t)(r1[b] >> 8));
-                const uint32_t j = (i0 + b) * kWave + lane;
-                const int32_t P = G.Pbase + 16 * (int32_t)j;
-                const int32_t lo = P > G.O ? P : G.O;
-                const int32_t hi = P + 16 < G.Ecap ? P + 16 : G.Ecap;
-                if (LZ4MI_ABLATE != 4) {
-                    if (lo == P && hi == P + 16) out16(c.dst + P, v);
-                    else store_range(c.dst + P, v, lo - P, hi - P);
-                }
-                pend &= ~(1u << (i0 + b));
-                stored |= 1u << (i0 + b);
-            }
-        }
-        if (!__ballot(pend != 0)) break;
-        if (!__ballot(stored != 0)) return false;
-        wait_vmem();       // this round's stores are complete before later rounds read them
-        for (uint32_t i = 0; i < nrows; ++i) {
-            const uint64_t bal = __ballot((stored >> i) & 1u);
-            if (bal && lane == 0) ((uint64_t*)S.pms)[i] |= bal;
-        }
-        __syncthreads();
-    }
-    return true;
 }
 
 __device__ __forceinline__ void decompress_block(const DecArgs& a) {
@@ -1328,18 +1115,14 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         const uint32_t lbase = lincl - run;
         const int64_t total = uniform(__shfl(lincl, kWave - 1, kWave));
         uint32_t first_err = 0xFFFFFFFFu;
-        bool plain = true;    // every match >= 16 bytes, not overlapping itself, source >= 16 bytes into the buffer
         for (uint32_t k = base; k < base + cnt; ++k) {
             const int64_t os = c.O + lbase + S.t_out[k];
             S.t_out[k] = (uint32_t)os;
             const SeqInfo q = seq_info(S, k);
             const uint32_t e = seq_error(c, os, (int64_t)c.ip + q.lit, q.ll, q.off, q.ml);
             if (e && first_err == 0xFFFFFFFFu) first_err = (k << 3) | e;
-            plain = plain && (q.ml == 0 || (q.ml >= 16 && q.off >= q.ml && c.out_off + os + q.ll - q.off >= 16));
         }
         first_err = wave_min(first_err);
-        // piece output for this table: plain matches and at most kLim pieces of output
-        const bool piece_ok = LZ4MI_PIECES && __ballot(!plain) == 0 && total + 16 <= 16 * (int64_t)kLim;
         __syncthreads();
         if (first_err != 0xFFFFFFFFu) { status = err_status(first_err & 7); break; }
 
@@ -1413,7 +1196,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         wait_vmem();
         settle(pf0);    // (so the next chunk's stage does not wait for this chunk's stores)
         settle(pf1);
-        if (!(piece_ok && piece_output(c, S, lane, nseq, total))) {
         // output -> sequence map for remap_src, in the (now idle) next-token table
         uint32_t msh = 4;
         while ((total >> msh) >= kLim) ++msh;
@@ -1526,7 +1308,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             }
             __syncthreads();
         }
-        }   // general output
         PROF(6);
         if (cut) {
             PROF_COUNT(12, 1);

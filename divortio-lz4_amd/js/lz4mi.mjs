@@ -226,13 +226,25 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
             pos = end;
         }
     } else {
-        // Dependent blocks (the reference's default): one table carried across blocks.
-        while (pos < end) {
-            const n = Math.min(bsize, end - pos);
-            const scratch = new Uint8Array(n + ((n / 255) | 0) + 16);
-            const c = native.compressBlock(work, scratch, pos, n, table, 0);
-            emit(pos, n, c, scratch.subarray(0, Math.max(0, Math.min(c, scratch.length))));
-            pos += n;
+        // Dependent blocks (the reference's default): one table carried across blocks, the
+        // whole chain in one GPU call (each block exactly compressBlock(work, scratch, pos, n,
+        // table, 0), the table updated in place).
+        const nb = Math.ceil((end - pos) / bsize);
+        if (nb > 0) {
+            const outOff = new Float64Array(nb), compLen = new Uint32Array(nb);
+            let slot = 0;
+            for (let b = 0; b < nb; b++) {
+                const n = Math.min(bsize, end - pos - b * bsize);
+                outOff[b] = slot;
+                slot += n + ((n / 255) | 0) + 16;
+            }
+            const scratch = new Uint8Array(slot);
+            native.compressChain(work, pos, end - pos, bsize, table, scratch, outOff, compLen);
+            for (let b = 0; b < nb; b++) {
+                const n = Math.min(bsize, end - pos);
+                emit(pos, n, compLen[b], scratch.subarray(outOff[b], outOff[b] + compLen[b]));
+                pos += n;
+            }
         }
     }
     if (blockChecksum && sums.length > 0) {

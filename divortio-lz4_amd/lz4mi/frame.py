@@ -152,6 +152,25 @@ def _shm_dir():
     return "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
 
 
+def _host_pieces(t, piece=_STAGE_PIECE, nbuf=4):
+    """Numpy views of consecutive pieces of a 1-D uint8 tensor. A device tensor goes through
+    `nbuf` rotating pinned buffers (full-rate device-to-host copies); a piece's buffer is
+    reused `nbuf` pieces later, after _ChecksumWorker (at most 3 pieces queued or in
+    hand) has finished with it."""
+    import torch
+    n = t.numel()
+    if t.device.type != "cuda":
+        for p in range(0, n, piece):
+            yield t[p:p + piece].numpy()
+        return
+    bufs = [torch.empty(min(piece, n), dtype=torch.uint8, pin_memory=True) for _ in range(min(nbuf, -(-n // piece)))]
+    for k, p in enumerate(range(0, n, piece)):
+        m = min(piece, n - p)
+        b = bufs[k % len(bufs)][:m]
+        b.copy_(t[p:p + m])
+        yield b.numpy()
+
+
 def staged_checksum(shard, group=None, root=0, seed=0):
     """XXH32 (the reference's variant, 64-bit length) of every rank's shard concatenated in
     rank order, computed on root's host: the content checksum is one serial chain,
@@ -165,8 +184,8 @@ def staged_checksum(shard, group=None, root=0, seed=0):
     n = shard.numel()
     if not multi:
         w = _ChecksumWorker(seed)
-        for p in range(0, n, _STAGE_PIECE):
-            w.feed(shard[p:p + _STAGE_PIECE].cpu().numpy())
+        for a in _host_pieces(shard):
+            w.feed(a)
         return w.digest()
     dev = shard.device
     t = torch.tensor([n], dtype=torch.int64, device=dev)
@@ -197,8 +216,8 @@ def staged_checksum(shard, group=None, root=0, seed=0):
     staged = False
     for r in range(world):
         if r == root:
-            for p in range(0, n, _STAGE_PIECE):
-                w.feed(shard[p:p + _STAGE_PIECE].cpu().numpy())
+            for a in _host_pieces(shard):
+                w.feed(a)
             continue
         if not staged:
             dist.barrier(group=group)
@@ -323,6 +342,9 @@ class DeviceDecoder:
         decoded bytes concatenated in order; status 0 or the reference's error code."""
         import torch
         import lz4mi
+        if rng.device.type != "cuda":          # a host frame: its bytes go to the current GPU once
+            rng = rng.to("cuda")
+            pay_rel, word = pay_rel.to("cuda"), word.to("cuda")
         dev = rng.device
         nb = pay_rel.numel()
         s = self.stream if self.stream is not None else torch.cuda.current_stream(dev)
@@ -356,9 +378,15 @@ class DeviceDecoder:
                 continue
             out[b * block_max:b * block_max + m].copy_(rng[p:p + m])
             out_len[b] = m
-        lens = out_len.to(torch.int64).tolist()
-        parts = [out[b * block_max:b * block_max + lens[b]] for b in range(nb)]
-        res = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8, device=dev)
+        if nb == 0:
+            return torch.zeros(0, dtype=torch.uint8, device=dev), status
+        # every block but the last filled its slot (the reference encoder's layout): the slots
+        # are the output already; otherwise close the gaps
+        lens = out_len.to(torch.int64)
+        if bool((lens[:-1] == block_max).all()):
+            return out[:(nb - 1) * block_max + int(lens[-1])], status
+        ll = lens.tolist()
+        res = torch.cat([out[b * block_max:b * block_max + ll[b]] for b in range(nb)])
         return res, status
 
 
@@ -382,6 +410,10 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     import torch
     import lz4mi
     dist, multi, world, rank = _dist_ctx(group)
+    if isinstance(frame, np.ndarray):
+        frame = torch.from_numpy(np.ascontiguousarray(frame, dtype=np.uint8))
+        if device is None and not multi:
+            device = frame.device
     if device is not None:
         dev = torch.device(device)
     elif frame is not None:
@@ -444,9 +476,9 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
         rng = frame[a:b]
     t0 = _phase(timings, "scatter", t0, dev)
     # ---- decode this rank's run
+    # each block decodes into block_max bytes (a block's output position depends on the sizes
+    # before it, which only the decode gives); the content size is checked on the sum below
     last_cap = bmax
-    if hi == nb and nb and csize > 0:
-        last_cap = max(0, min(bmax, csize - (nb - 1) * bmax))
     out, status = decoder.decode(rng, pay[lo:hi] - a, word[lo:hi], bmax, last_cap)
     bad = torch.nonzero(status != 0).flatten()
     first = torch.tensor([lo + int(bad[0]) if bad.numel() else nb, int(status[bad[0]]) if bad.numel() else 0],
@@ -455,9 +487,14 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
         allf = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
         dist.all_gather(allf, first, group=group)
         first = min(allf, key=lambda x: int(x[0]))
+    total = torch.tensor([out.numel()], dtype=torch.int64, device=dev)
+    if multi:
+        dist.all_reduce(total, group=group)
     t0 = _phase(timings, "kernel", t0, dev)
     if int(first[0]) < nb:
         raise lz4mi.Lz4miError(int(first[1]))
+    if csize > 0 and int(total.item()) != csize:
+        raise lz4mi.Lz4miError(lz4mi.ERR_MALFORMED, "lz4mi: decoded size differs from the frame's content size")
     # ---- content checksum from host-staged shards (before the gather: the shards are local)
     if verify_checksum and flg & 0x04:
         d = staged_checksum(out, group, root)

@@ -245,6 +245,47 @@ static napi_value n_compress_blocks(napi_env env, napi_callback_info info) {
     return make_i64(env, 0);
 }
 
+/* compressChain(src, start, len, blockSize, hashTable, out, outOff, compLen) -> 0: the dependent
+ * blocks of one frame in one GPU chain (lz4mi_compress_chain) */
+static napi_value n_compress_chain(napi_env env, napi_callback_info info) {
+    size_t argc = 8;
+    napi_value argv[8];
+    CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    view_t src, tab, out, ooff, clen;
+    int64_t start, len, bs;
+    if (!get_view(env, argv[0], &src, 1, "src") || !get_i64(env, argv[1], &start) || !get_i64(env, argv[2], &len) ||
+        !get_i64(env, argv[3], &bs) || !get_view(env, argv[4], &tab, 1, "hashTable") ||
+        !get_view(env, argv[5], &out, 1, "out") || !get_view(env, argv[6], &ooff, 1, "outOff") ||
+        !get_view(env, argv[7], &clen, 1, "compLen"))
+        return NULL;
+    if (tab.type != napi_int32_array || tab.length < 16384) {
+        napi_throw_type_error(env, NULL, "lz4mi: hashTable must be an Int32Array(16384)");
+        return NULL;
+    }
+    if (start < 0 || len < 0 || bs <= 0 || bs > LZ4MI_MAX_BLOCK || !in_bounds((uint64_t)start, (uint64_t)len, src.length))
+        return throw_status(env, LZ4MI_ERR_ARG);
+    const uint32_t n = (uint32_t)((len + bs - 1) / bs);
+    if (!u32_array(env, &clen, n, 0, "compLen")) return NULL;
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+    if (!offs) return throw_status(env, LZ4MI_ERR_ARG);
+    if (!f64_offsets(env, &ooff, n, offs, "outOff")) {
+        free(offs);
+        return NULL;
+    }
+    for (uint32_t b = 0; b < n; ++b) {
+        const uint64_t nb = (uint64_t)(len - (int64_t)b * bs) < (uint64_t)bs ? (uint64_t)(len - (int64_t)b * bs) : (uint64_t)bs;
+        if (!in_bounds(offs[b], lz4mi_compress_bound(nb), out.length)) {
+            free(offs);
+            return throw_status(env, LZ4MI_ERR_ARG);
+        }
+    }
+    int32_t st = lz4mi_compress_chain((const uint8_t*)src.data, src.length, (int32_t)start, (int32_t)len, (int32_t)bs,
+                                      (int32_t*)tab.data, (uint8_t*)out.data, offs, (uint32_t*)clen.data, 0, NULL);
+    free(offs);
+    if (st) return throw_status(env, st);
+    return make_i64(env, 0);
+}
+
 /* decompressBlocks(input, inOff, inLen, output, outOff, outCap, outLen, status, dictionary?, flags?) -> status */
 static napi_value n_decompress_blocks(napi_env env, napi_callback_info info) {
     size_t argc = 10;
@@ -439,6 +480,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"compressBlock", NULL, n_compress_block, NULL, NULL, NULL, napi_default, NULL},
         {"decompressBlock", NULL, n_decompress_block, NULL, NULL, NULL, napi_default, NULL},
         {"compressBlocks", NULL, n_compress_blocks, NULL, NULL, NULL, napi_default, NULL},
+        {"compressChain", NULL, n_compress_chain, NULL, NULL, NULL, napi_default, NULL},
         {"decompressBlocks", NULL, n_decompress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"xxHash32", NULL, n_xxh32, NULL, NULL, NULL, napi_default, NULL},
         {"xxh32Reset", NULL, n_xxh32_reset, NULL, NULL, NULL, napi_default, NULL},

@@ -204,6 +204,19 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
                                uint32_t flags, void* stream);
 
 /*
+ * Dependent blocks of one frame (the reference's LZ4.compress default,
+ * src/buffer/bufferCompress.js:182-236, which calls compressBlock once per block with one
+ * table): block b = src[start + b*block_size, ...) compressed in order on one GPU chain with
+ * `table` (Int32Array(16384) semantics, in/out, positions absolute in src) carried across
+ * blocks; block b's bytes go to out + out_off[b] (room for lz4mi_compress_bound(n_b)),
+ * comp_len[b] = its size, exactly compressBlock(src, scratch, start_b, n_b, table, 0). One
+ * launch for the whole frame (one staging of src and the table). Host pointers only.
+ */
+int32_t lz4mi_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len, int32_t block_size,
+                             int32_t* table, uint8_t* out, const uint64_t* out_off, uint32_t* comp_len, uint32_t flags,
+                             void* stream);
+
+/*
  * Block index of a device-resident frame, for decoding its blocks on several devices
  * (the block walk of bufferDecompress.js:133-192 without decoding): one lane walks the
  * header and the size words and writes, per block in frame order, the payload position

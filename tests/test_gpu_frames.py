@@ -53,8 +53,32 @@ def test_config4_complete_frame_64mib():
     torch.cuda.synchronize()
     assert got.numel() == ref.size
     assert np.array_equal(got.cpu().numpy(), ref)
-    back = F.decompress_frame_sharded(ref, verify_checksum=True)
-    assert np.array_equal(back.numpy(), host)
+    back = F.decompress_frame_sharded(got, verify_checksum=True)          # device frame: index on the GPU
+    assert back.is_cuda and np.array_equal(back.cpu().numpy(), host)
+    tim = {}
+    back = F.decompress_frame_sharded(ref, verify_checksum=True, timings=tim)   # host frame
+    assert np.array_equal(back.cpu().numpy(), host)
+    assert {"index", "scatter", "kernel", "checksum"} <= set(tim)
+    # the block index of a ragged frame (4 + 4 + 4 + 3 MiB)
+    part = host[:5 * (3 << 20)]
+    odd = O.compress_frame(part, None, BLOCK, True, True, True)
+    idx_meta, pay, word = F.frame_index(torch.from_numpy(odd).cuda())
+    assert idx_meta["content_size"] == part.size and pay.numel() == 4
+    assert np.array_equal(F.decompress_frame_sharded(odd).cpu().numpy(), part)
+    # a middle block that does not fill block_max (another encoder's layout: 4, 1, 4 MiB):
+    # the outputs are compacted, not laid out at block_max strides
+    from lz4mi import shard
+    pieces = [host[:BLOCK], host[BLOCK:BLOCK + (1 << 20)], host[2 * BLOCK:3 * BLOCK]]
+    want = np.concatenate(pieces)
+    body = shard.block_records(pieces, [O.compress_block_bytes(x) for x in pieces])
+    fr = np.concatenate([np.frombuffer(F.header(BLOCK, True, True, want.size), dtype=np.uint8), body,
+                         np.zeros(4, dtype=np.uint8), np.array([O.xxh32(want)], dtype="<u4").view(np.uint8)])
+    assert np.array_equal(F.decompress_frame_sharded(torch.from_numpy(fr).cuda()).cpu().numpy(), want)
+    corrupt = got.clone()
+    corrupt[-1] ^= 0x5A
+    with pytest.raises(lz4mi.Lz4miError) as ei:
+        F.decompress_frame_sharded(corrupt, verify_checksum=True)
+    assert str(ei.value) == "LZ4: Content Checksum Error"
 
 
 def test_frame_with_block_checksums_matches_oracle():

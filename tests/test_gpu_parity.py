@@ -281,3 +281,29 @@ def test_frame_pack_matches_reference_frame():
                          comp_len.data_ptr(), out.data_ptr(), rec_off.data_ptr(), nb, s)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref[first:ref.size - 4])
+
+
+@pytest.mark.parametrize("bs", [65536, 262144, 1 << 20])
+def test_compress_chain_dependent_blocks_match_oracle(bs):
+    """lz4mi_compress_chain (the dependent-block frame mode in one GPU chain, source ring in
+    LDS): every block == the oracle's compressBlock(src, scratch, start_b, n_b, table, 0) with
+    the table carried, and the final table equal — on mixed data (matches across block
+    boundaries, incompressible runs, long repetitive runs past the ring's look-ahead), from a
+    start past a 64 KiB history and with a non-empty incoming table."""
+    data = np.concatenate([O.generate("text", 41, 300000), O.generate("tiles216", 42, 700000),
+                           O.generate("random", 43, 200000), O.generate("repetitive", 44, 500000),
+                           O.generate("copy", 45, 400000)])
+    for start, init in ((0, 0), (100000, -1), (70001, 5)):
+        length = data.size - start - 12345
+        t_ref = np.full(16384, init, dtype=np.int32)
+        t_gpu = t_ref.copy()
+        got = lz4mi.compress_chain(data, start, length, bs, t_gpu)
+        pos, b = start, 0
+        while pos < start + length:
+            n = min(bs, start + length - pos)
+            w, out, _ = O.compress_block(data, pos, n, t_ref)
+            assert np.array_equal(got[b], out[:w]), (bs, start, b)
+            pos += n
+            b += 1
+        assert b == len(got)
+        assert np.array_equal(t_gpu, t_ref), (bs, start)

@@ -10,10 +10,10 @@ C=$R/divortio-lz4_amd/csrc
 T=$(mktemp -d)
 cp $C/*.h $C/*.hip $C/*.cpp $T/
 F0=${FILE:-lz4mi_decompress.hip}
+[ -n "$SRCFILE" ] && cp "$SRCFILE" $T/$F0   # a whole replacement source for $F0 (e.g. from git show)
 sed -i "$expr" $T/$F0
 mkdir -p $R/tools/variants
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include $*"
-objs=""
 objs=""
 for f in lz4mi_decompress.hip lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_frame.hip lz4mi_capi.cpp; do
   if [ "$f" = "$F0" ]; then srcf=$T/$f; else srcf=$C/$f; fi
