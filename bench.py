@@ -246,6 +246,26 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
     }
 
 
+def weak_scaling(torch, dist, walls, kern_s, bytes_per_rank, steps, device):
+    """The bench's aggregation: every rank's timed-region wall times (`walls`, seconds) are
+    max-reduced, value = all ranks' bytes / the slowest rank's wall (weak scaling: each rank
+    has its own fixed batch); the per-rank kernel times are gathered so imbalance (the
+    skewed mix) shows. Returns (max walls, value GB/s, per-rank kernel ms lists)."""
+    world = dist.get_world_size() if dist is not None else 1
+    t = torch.tensor(list(walls), dtype=torch.float64, device=device)
+    k = torch.tensor(list(kern_s), dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ks = [torch.zeros_like(k) for _ in range(world)]
+        dist.all_gather(ks, k)
+    else:
+        ks = [k]
+    mx = [float(x) for x in t.tolist()]
+    value = world * bytes_per_rank * steps / mx[0] / 1e9
+    per_rank = [[round(float(x) * 1e3, 3) for x in kk.tolist()] for kk in ks]
+    return mx, value, [list(col) for col in zip(*per_rank)]
+
+
 def cpu_threads():
     """The host cores this job may use: the box exports OMP_NUM_THREADS (its CPU share)."""
     n = os.environ.get("OMP_NUM_THREADS")
@@ -391,14 +411,12 @@ def main():
     d_wall, d_kern = timed(torch, dist, lambda: batch.decompress(lz4mi, stream), args.steps, args.warmup, stream_obj)
     ok = batch.verify(torch, lz4mi, stream)
 
-    t = torch.tensor([d_wall, c_wall], dtype=torch.float64, device="cuda")
     okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device="cuda")
     if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(okt, op=dist.ReduceOp.MAX)
-    d_wall, c_wall = float(t[0]), float(t[1])
+    (d_wall, c_wall), value, per_rank_ms = weak_scaling(torch, dist, (d_wall, c_wall), (d_kern, c_kern), raw_bytes,
+                                                        args.steps, "cuda")
     ms_per_step = d_wall / args.steps * 1e3
-    value = world * raw_bytes * args.steps / d_wall / 1e9
 
     napi = napi_e2e(batch) if args.napi and rank == 0 and world == 1 else None
     c_base = c_cpu_baseline(batch, cpu_threads()) if args.cpu_baseline and rank == 0 and world == 1 else None
@@ -467,6 +485,8 @@ def main():
     }
     if traffic_src:
         line["roofline"]["traffic_source"] = traffic_src
+    if world > 1:   # every rank's average launch time: the imbalance the max hides
+        line["per_rank_kernel_ms"] = {"decompress": per_rank_ms[0], "compress": per_rank_ms[1]}
     if frame is not None:
         line["frame"] = frame
     if extra:

@@ -262,6 +262,10 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
     int64_t i = j.start, anchor = j.start, op = j.dst_pos;
     uint32_t miss = 67;
     // 128-byte source window [wi, wi+128): lane k holds bytes wi+k and wi+64+k
+#if LZ4MI_CPROFILE
+    uint64_t cprof[10] = {0};
+    uint64_t cprof_t = wall_clock64();
+#endif
     if (RING) ring_advance(j, *rg, lane, i);
     int64_t wi = i;
     uint32_t wlo = sbyte<RING>(j, *rg, wi + lane), whi = sbyte<RING>(j, *rg, wi + 64 + lane);
@@ -279,14 +283,18 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         uint32_t seq = win_byte(wlo, whi, k0) | (win_byte(wlo, whi, k0 + 1) << 8) |
                        (win_byte(wlo, whi, k0 + 2) << 16) | (win_byte(wlo, whi, k0 + 3) << 24);
         uint32_t h = (seq * kP1) >> 18;
+        CPROF(0);
+        CPROF_COUNT(8, 1);
         int32_t cand = T[h] - 1;
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) T[h] = (int32_t)i + 1;
         cand = __builtin_amdgcn_readfirstlane(cand);
         if (cand < 0 || cand == i || ((uint32_t)(i - cand) >> 16) != 0) {
             i += miss++ >> 6;
+            CPROF(1);
             continue;
         }
+        CPROF(1);
         // fetch the candidate's 128 bytes and re-anchor the window at i, one round trip
         wi = i;
         wlo = sbyte<RING>(j, *rg, i + lane);
@@ -296,8 +304,11 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         settle32(wlo);
         if (neq_lo & 0xFull) {                    // the 4-byte content check failed
             i += miss++ >> 6;
+            CPROF(2);
             continue;
         }
+        CPROF(2);
+        CPROF_COUNT(9, 1);
         miss = 67;
         // forward extension: e = i+4.. while e < matchlimit and bytes equal
         int64_t lim = matchlimit - i;             // compare bytes k in [4, lim)
@@ -329,6 +340,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
                 }
             }
         }
+        CPROF(3);
         int64_t mcode = e - i - 4;
         int64_t lit = i - anchor;
         op = emit_literals<RING>(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range, rg);
@@ -345,7 +357,12 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         }
         i = e;
         anchor = e;
+        CPROF(4);
     }
+#if LZ4MI_CPROFILE
+    if (lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
+#endif
     op = emit_literals<RING>(j, lane, op, anchor, end - anchor, 0, range, rg);
     return op - j.dst_pos;
 }
@@ -740,7 +757,7 @@ __global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
 // the CU's L1 sees the wave's own completed stores (nontemporal loads and an
 // atomic exchange at the head, used until round 2, cost 7 %: 208.8 vs 194.5 ms).
 #ifndef LZ4MI_GT16
-#define LZ4MI_GT16 0   // 1: the batch encoder's tables as 15-bit positions in global + 2-bit epoch codes in LDS
+#define LZ4MI_GT16 1   // 1: the batch encoder's tables as 15-bit positions in global + 2-bit epoch codes in LDS
 #endif
 
 struct GtShared {

@@ -434,34 +434,14 @@ __device__ __forceinline__ uint4 load16(const Ctx& c, const DecShared& S, int32_
     return v;
 }
 
-// A lane's 16 bytes of a sink for the pipelines' empty slots. With the copy pipelines'
-// loads and stores under `if`, a branch may skip them, the compiler cannot count the
-// wave's outstanding vector-memory ops, and every use of a loaded value waited with
-// vmcnt(0) — for all loads and stores in flight, including the next stage's loads the
-// pipeline had just issued. Unconditional loads and stores (an empty slot reads and
-// writes here) keep the counts static: a store waits only for its own stage's loads.
-__device__ uint4 g_dec_sink[kWave];
-__device__ __forceinline__ uint8_t* sink16() { return (uint8_t*)&g_dec_sink[threadIdx.x]; }
-
 template <uint32_t KIND, bool TWO, int NB>
 __device__ __forceinline__ void load_slots(const Ctx& c, const DecShared& S, const Slot (&s)[NB], uint4 (&A)[NB],
                                            uint4 (&B)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         if (LZ4MI_ABLATE == 5) { A[j] = make_uint4(0, 0, 0, 0); B[j] = A[j]; continue; }
-        if (KIND == R_LDS) {
-            if (s[j].wm >> 8) A[j] = load16<KIND>(c, S, s[j].a);
-        } else {
-            const uint8_t* base = KIND == R_COMP ? c.blk : c.dst;
-            const uint8_t* pa = (s[j].wm >> 8) ? base + s[j].a : sink16();
-            const u32x4_t t = *(const u32x4_t*)pa;
-            A[j] = make_uint4(t.x, t.y, t.z, t.w);
-            if (TWO) {
-                const uint8_t* pb = (s[j].wm >> 8) == 2 ? base + s[j].a - s[j].per : sink16();
-                const u32x4_t u = *(const u32x4_t*)pb;
-                B[j] = make_uint4(u.x, u.y, u.z, u.w);
-            }
-        }
+        if (s[j].wm >> 8) A[j] = load16<KIND>(c, S, s[j].a);
+        if (TWO && (s[j].wm >> 8) == 2) B[j] = load16<KIND>(c, S, s[j].a - s[j].per);
     }
 }
 
@@ -470,16 +450,18 @@ __device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Sl
                                             const uint4 (&B)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        // pipe() takes runs of >= 16 bytes only (wave runs): every piece is 16 bytes wide
         const uint32_t mode = s[j].wm >> 8;
+        if (!mode) continue;
         uint4 v = A[j];
         if (TWO && mode == 2) v = pick4(A[j], B[j], s[j].k);
         else if (mode == 3) v = expand_period(A[j], s[j].k, s[j].per);
         if (LZ4MI_ABLATE == 4) {      // timing only: loads kept alive, no stores
-            if (mode && (v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pms[0] = 1;
+            if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
-        out16(mode ? c.dst + s[j].y : sink16(), v);
+        const uint32_t w = s[j].wm & 255u;
+        if (w == 16) out16(c.dst + s[j].y, v);
+        else store_w(c.dst + s[j].y, v, w);
     }
 }
 
@@ -596,16 +578,14 @@ struct LaneMatchGen {
     }
 };
 
-// Every slot loads and stores, an empty one from / to this lane's 16 bytes of a sink
-// (g_dec_sink): with no branch around them the compiler can count the wave's outstanding
-// vector-memory ops and wait only for the stage a store needs.
 template <int NB>
 __device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], uint4 (&A)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        const uint8_t* p = s[j].w ? c.dst + s[j].a : sink16();
-        const u32x4_t t = *(const u32x4_t*)p;
-        A[j] = make_uint4(t.x, t.y, t.z, t.w);
+        if (s[j].w) {
+            const u32x4_t t = *(const u32x4_t*)(c.dst + s[j].a);
+            A[j] = make_uint4(t.x, t.y, t.z, t.w);
+        }
     }
 }
 
@@ -613,12 +593,12 @@ template <int NB>
 __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+        if (!s[j].w) continue;
         if (LZ4MI_ABLATE == 4) {
-            if (s[j].w && (A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;
+            if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;
             continue;
         }
-        uint8_t* p = s[j].w ? c.dst + s[j].y : sink16();
-        out16(p, A[j]);
+        out16(c.dst + s[j].y, A[j]);
     }
 }
 
@@ -734,26 +714,9 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
     }
 }
 
-// A run shorter than 16 bytes (only the cut sequence's runs reach wave_run that short):
-// lane t copies byte t; every source byte is final (non-periodic: the source ends at or
-// before y; periodic: [src, src + period) lies before y).
-__device__ __forceinline__ void small_run(const Ctx& c, const DecShared& S, int lane, const Run& R) {
-    if (lane >= R.n) return;
-    const int32_t t = R.period ? lane % R.period : lane;
-    uint32_t v;
-    if (R.kind == R_LDS) v = ((const uint8_t*)S.stage)[R.src + lane];
-    else if (R.kind == R_COMP) v = c.blk[R.src + lane];
-    else v = hist_byte(c, (int64_t)R.src + t);
-    c.dst[R.y + lane] = (uint8_t)v;
-}
-
 // The whole wave writes one run (uniform R).
 __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, const Run& R, PatBuf B) {
     if (R.kind == R_NONE || R.n <= 0) return;
-    if (R.n < 16) {          // pipe() writes whole 16-byte pieces
-        small_run(c, S, lane, R);
-        return;
-    }
     // (a byte-wise periodic run whose source is inside the buffer qualifies too:
     // periodic_run reads only [src, src + period))
     const bool in_buf = R.kind == R_HIST || (R.kind == R_BYTES && c.out_off + R.src >= 0);
@@ -791,8 +754,8 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         const uint4 v0 = stage16(S.stage, L.src + d0);
         const uint4 v1 = stage16(S.stage, L.src + d1);
         if (LZ4MI_ABLATE == 4) continue;
-        out16(q < np ? c.dst + L.y + d0 : sink16(), v0);
-        out16(q + 1 < np ? c.dst + L.y + d1 : sink16(), v1);
+        if (q < np) out16(c.dst + L.y + d0, v0);
+        if (q + 1 < np) out16(c.dst + L.y + d1, v1);
     }
     if (__ballot(n > 0 && n < 16)) {                       // shorter runs: two overlapping 8/4/2/1-byte stores
         if (n > 0 && n < 16) {

@@ -235,3 +235,55 @@ def test_frame_gather_and_sharded_decode_world2():
     assert sorted(r[0] for r in res) == [0, 1]
     for r in res:
         assert r[1] is True and r[2] is True, r
+
+
+def _scaling_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "divortio-lz4_amd")]
+    import importlib.util
+    import torch
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+        bench = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(bench)
+        from lz4mi import shard
+        n_total = 16
+        mine = shard.shard_interleaved(n_total, rank, world)
+        kinds = shard.clustered_mix_kinds(n_total)
+        # a stand-in timing: random blocks cost 1, tiles216 blocks 3 (the skew the interleave evens out)
+        kern = sum(1.0 if kinds[b] == "random" else 3.0 for b in mine) / 1000.0
+        wall = kern * 5 + 0.001 * rank
+        walls, value, per_rank = bench.weak_scaling(torch, dist, (wall, 2 * wall), (kern, 2 * kern),
+                                                    len(mine) * (4 << 20), 5, "cpu")
+        q.put((rank, walls, value, per_rank, kern))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
+
+
+def test_weak_scaling_value_formula_world2():
+    """bench.py's aggregation at world 2 on the clustered mix dealt out interleaved: the
+    walls are max-reduced on every rank, value = all ranks' bytes x steps / the slowest wall,
+    and every rank's kernel time is reported (equal shares of each cluster: balanced)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_scaling_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[2] is not None for r in res), res
+    kerns = [r[4] for r in res]
+    walls = [k * 5 + 0.001 * i for i, k in enumerate(kerns)]
+    for rank, mx, value, per_rank, _ in res:
+        assert abs(mx[0] - max(walls)) < 1e-12 and abs(mx[1] - 2 * max(walls)) < 1e-12
+        assert abs(value - 2 * 8 * (4 << 20) * 5 / max(walls) / 1e9) < 1e-6
+        assert per_rank[0] == [round(k * 1e3, 3) for k in kerns]
+    assert kerns[0] == kerns[1]          # interleaving gave both ranks the same mix
