@@ -361,10 +361,11 @@ def reference_benchmark(with_js):
     return out
 
 
-def pmc_traffic(lz4mi, n, gen):
-    """HBM bytes per decode launch from the committed rocprofv3 PMC passes, used only when
-    they were measured on this exact build and workload (else null)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(lz4mi, n, gen, name="pmc_traffic.json"):
+    """HBM bytes per launch (decode: pmc_traffic.json, compress: pmc_traffic_compress.json)
+    from the committed rocprofv3 PMC passes, used only when they were measured on this exact
+    build and workload (else null)."""
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             pm = json.load(f)
@@ -452,6 +453,7 @@ def main():
             frame = {"error": repr(e)[-500:]}
     achieved = (raw_bytes + comp_bytes) / d_kern / 1e9
     traffic, traffic_src = pmc_traffic(lz4mi, n, args.gen)
+    c_traffic, _ = pmc_traffic(lz4mi, n, args.gen, "pmc_traffic_compress.json")
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -478,8 +480,9 @@ def main():
                     "round trip (compress then decompress of the same bytes) are under 'compress' and "
                     "'roundtrip_GBps'",
         "compress": {"GBps": round(world * raw_bytes / c_wall * args.compress_steps / 1e9, 2),
-                     "kernel_ms": round(c_kern * 1e3, 3),
-                     "hbm_frac": round((raw_bytes + comp_bytes) / c_kern / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "kernel": "lz4mi_compress_gt_kernel", "kernel_ms": round(c_kern * 1e3, 3),
+                     "hbm_frac": round((raw_bytes + comp_bytes) / c_kern / 1e9 / HBM_PEAK_GBPS, 4),
+                     "algorithmic_bytes_per_launch": raw_bytes + comp_bytes, "traffic": c_traffic},
         "roundtrip_GBps": round(world * raw_bytes / (c_wall / args.compress_steps + d_wall / args.steps) / 1e9, 2),
         "build_id": lz4mi.build_id(),
     }

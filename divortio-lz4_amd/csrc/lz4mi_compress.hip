@@ -74,61 +74,14 @@ __device__ __forceinline__ uint32_t win_byte(uint32_t lo, uint32_t hi, uint32_t 
     return k < 64 ? __builtin_amdgcn_readlane(lo, k) : __builtin_amdgcn_readlane(hi, k - 64);
 }
 
-// ---- source ring of the dependent-block chain (lz4mi_compress_chain): the last
-// 64 KiB of the parse plus up to 32 KiB ahead of it, in LDS, so a probe's window,
-// the candidate's bytes and the literal copies are LDS reads instead of global
-// round trips (the chain is one wave's serial walk: its latency is the speed).
-// Byte p (absolute) lives at g_ring[p mod kRingBytes] while p in [lo, hi).
-constexpr uint32_t kRingBytes = 96 * 1024;
-constexpr int64_t kRingStep = 16 * 1024;     // refill granularity (16-byte aligned pieces)
-constexpr int64_t kRingAhead = 4096;         // refill when fewer bytes than this are ahead of the parse
-static_assert(kRingBytes - 65536 >= kRingStep + kRingAhead, "a refill never evicts a byte a probe can reach");
-__shared__ uint8_t g_ring[kRingBytes];
-
-struct Ring {
-    int64_t lo, hi;
-};
-
-template <bool RING>
-__device__ __forceinline__ uint32_t sbyte(const CompJob& j, const Ring& r, int64_t p) {
-    if (RING && p >= r.lo && p < r.hi) return g_ring[(uint32_t)p % kRingBytes];
-    return src_byte(j, p);
-}
-
-// Bring at least kRingAhead bytes ahead of position i into the ring (whole wave).
-__device__ void ring_advance(const CompJob& j, Ring& r, int lane, int64_t i) {
-    while ((uint64_t)r.hi < j.src_total && r.hi - i < kRingAhead + 256) {
-        const int64_t n = (int64_t)j.src_total - r.hi < kRingStep ? (int64_t)j.src_total - r.hi : kRingStep;
-        for (int64_t k = 16 * lane; k < n; k += 16 * kWave) {
-            const int64_t p = r.hi + k;
-            const uint32_t q = (uint32_t)p % kRingBytes;
-            if (k + 16 <= n) {
-                uint4 v;
-                __builtin_memcpy(&v, j.src + p, 16);
-                *(uint4*)&g_ring[q] = v;
-            } else {
-                for (int64_t t = 0; k + t < n; ++t) g_ring[q + t] = j.src[p + t];
-            }
-        }
-        __syncthreads();
-        r.hi += n;
-        if (r.hi - r.lo > (int64_t)kRingBytes) r.lo = r.hi - kRingBytes;
-    }
-}
-
 // dst[p, p+n) = v (wave-parallel).
 __device__ void wave_fill(const CompJob& j, int lane, int64_t p, int64_t n, uint32_t v) {
     for (int64_t k = lane; k < n; k += kWave) put_byte(j, p + k, v);
 }
 
 // dst[d, d+n) = src[s, s+n) (wave-parallel, aligned dword stores where possible).
-template <bool RING = false>
-__device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int64_t n, const Ring* rg = nullptr) {
+__device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int64_t n) {
     if (n <= 0) return;
-    if (RING && s >= rg->lo && s + n <= rg->hi) {     // literals in the ring: LDS reads, byte stores in order
-        for (int64_t k = lane; k < n; k += kWave) put_byte(j, d + k, g_ring[(uint32_t)(s + k) % kRingBytes]);
-        return;
-    }
     uintptr_t da = (uintptr_t)(j.dst + d);
     int64_t head = (int64_t)((4 - (da & 3)) & 3);
     if (head > n) head = n;
@@ -171,6 +124,63 @@ __device__ __forceinline__ uint32_t ld_u32(const CompJob& j, int64_t p) {
         return v;
     }
     return src_byte(j, p) | (src_byte(j, p + 1) << 8) | (src_byte(j, p + 2) << 16) | (src_byte(j, p + 3) << 24);
+}
+
+// ---- source ring of the dependent-block chain (lz4mi_compress_chain): the last
+// 64 KiB of the parse plus up to 32 KiB ahead of it, in LDS, so a probe's window,
+// the candidate's bytes and the literal copies are LDS reads instead of global
+// round trips (the chain is one wave's serial walk: its latency is the speed).
+// Byte p (absolute) lives at g_ring[p mod kRingBytes] while p in [lo, hi).
+constexpr uint32_t kRingBytes = 88 * 1024;
+constexpr int64_t kRingStep = 16 * 1024;     // refill granularity (16-byte aligned pieces)
+constexpr int64_t kRingAhead = 4096;         // refill when fewer bytes than this are ahead of the parse
+static_assert(kRingBytes - 65536 >= kRingStep + kRingAhead, "a refill never evicts a byte a probe can reach");
+__shared__ uint8_t g_ring[kRingBytes];
+
+struct Ring {
+    int64_t lo, hi;
+};
+
+// Source readers: global (the batch kernels) or through the chain's ring.
+struct SrcG {
+    __device__ static __forceinline__ uint32_t byte(const CompJob& j, const Ring*, int64_t p) { return src_byte(j, p); }
+    __device__ static __forceinline__ uint32_t u32(const CompJob& j, const Ring*, int64_t p) { return ld_u32(j, p); }
+};
+struct SrcR {
+    __device__ static __forceinline__ uint32_t byte(const CompJob& j, const Ring* r, int64_t p) {
+        if (p >= r->lo && p < r->hi) return g_ring[(uint32_t)p % kRingBytes];
+        return src_byte(j, p);
+    }
+    __device__ static __forceinline__ uint32_t u32(const CompJob& j, const Ring* r, int64_t p) {
+        if (p >= r->lo && p + 4 <= r->hi) {
+            const uint32_t q = (uint32_t)p % kRingBytes;
+            if (q <= kRingBytes - 4) return *(const uint32_t*)&g_ring[q];   // unaligned LDS dword (unaligned mode)
+            return g_ring[q] | (g_ring[(q + 1) % kRingBytes] << 8) | (g_ring[(q + 2) % kRingBytes] << 16) |
+                   ((uint32_t)g_ring[(q + 3) % kRingBytes] << 24);
+        }
+        return ld_u32(j, p);
+    }
+};
+
+// Bring at least kRingAhead bytes ahead of position i into the ring (whole wave).
+__device__ void ring_advance(const CompJob& j, Ring& r, int lane, int64_t i) {
+    while ((uint64_t)r.hi < j.src_total && r.hi - i < kRingAhead + 256) {
+        const int64_t n = (int64_t)j.src_total - r.hi < kRingStep ? (int64_t)j.src_total - r.hi : kRingStep;
+        for (int64_t k = 16 * lane; k < n; k += 16 * kWave) {
+            const int64_t p = r.hi + k;
+            const uint32_t q = (uint32_t)p % kRingBytes;
+            if (k + 16 <= n) {
+                uint4 v;
+                __builtin_memcpy(&v, j.src + p, 16);
+                *(uint4*)&g_ring[q] = v;
+            } else {
+                for (int64_t t = 0; k + t < n; ++t) g_ring[q + t] = j.src[p + t];
+            }
+        }
+        __syncthreads();
+        r.hi += n;
+        if (r.hi - r.lo > (int64_t)kRingBytes) r.lo = r.hi - kRingBytes;
+    }
 }
 
 // First differing byte of src[a + t] vs src[b + t], t in [0, lim) (lim if none).
@@ -223,9 +233,8 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
 // A run of more than 64 literals is one output.set() in the reference (blockCompress.js:100,
 // :198), which throws a RangeError instead of writing when the run does not fit: `range`
 // is set and the position after the length bytes returned (what was written stays).
-template <bool RING = false>
 __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t anchor, int64_t lit,
-                                 uint32_t mnib, bool& range, const Ring* rg = nullptr) {
+                                 uint32_t mnib, bool& range) {
     uint32_t tok = (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib;
     const int64_t tok_pos = op;
     if (lane == 0) put_byte(j, op, tok);
@@ -243,7 +252,7 @@ __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t
         range = true;
         return op;
     }
-    wave_copy<RING>(j, lane, op, anchor, lit, rg);
+    wave_copy(j, lane, op, anchor, lit);
     return op + lit;
 }
 
@@ -254,8 +263,7 @@ __device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t
 // the chain (the loads themselves completed long before).
 __device__ __forceinline__ void settle32(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
-template <bool RING = false>
-__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range, Ring* rg = nullptr) {
+__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range) {
     const int64_t end = (int64_t)j.start + j.len;
     const int64_t mflimit = end - 12;
     const int64_t matchlimit = end - 5;
@@ -266,16 +274,14 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
     uint64_t cprof[10] = {0};
     uint64_t cprof_t = wall_clock64();
 #endif
-    if (RING) ring_advance(j, *rg, lane, i);
     int64_t wi = i;
-    uint32_t wlo = sbyte<RING>(j, *rg, wi + lane), whi = sbyte<RING>(j, *rg, wi + 64 + lane);
+    uint32_t wlo = src_byte(j, wi + lane), whi = src_byte(j, wi + 64 + lane);
 
     while (i < mflimit) {
-        if (RING && rg->hi - i < kRingAhead) ring_advance(j, *rg, lane, i);
         if (i + 4 > wi + 128) {
             wi = i;
-            wlo = sbyte<RING>(j, *rg, wi + lane);
-            whi = sbyte<RING>(j, *rg, wi + 64 + lane);
+            wlo = src_byte(j, wi + lane);
+            whi = src_byte(j, wi + 64 + lane);
         }
         settle32(wlo);
         settle32(whi);
@@ -297,9 +303,9 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         CPROF(1);
         // fetch the candidate's 128 bytes and re-anchor the window at i, one round trip
         wi = i;
-        wlo = sbyte<RING>(j, *rg, i + lane);
-        whi = sbyte<RING>(j, *rg, i + 64 + lane);
-        uint32_t clo = sbyte<RING>(j, *rg, (int64_t)cand + lane), chi = sbyte<RING>(j, *rg, (int64_t)cand + 64 + lane);
+        wlo = src_byte(j, i + lane);
+        whi = src_byte(j, i + 64 + lane);
+        uint32_t clo = src_byte(j, (int64_t)cand + lane), chi = src_byte(j, (int64_t)cand + 64 + lane);
         uint64_t neq_lo = __ballot(wlo != clo);
         settle32(wlo);
         if (neq_lo & 0xFull) {                    // the 4-byte content check failed
@@ -329,8 +335,8 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
                         e = p + match_extent(j, lane, p, mp, matchlimit - p);
                         break;
                     }
-                    uint32_t a0 = sbyte<RING>(j, *rg, p + lane), a1 = sbyte<RING>(j, *rg, p + 64 + lane);
-                    uint32_t b0 = sbyte<RING>(j, *rg, mp + lane), b1 = sbyte<RING>(j, *rg, mp + 64 + lane);
+                    uint32_t a0 = src_byte(j, p + lane), a1 = src_byte(j, p + 64 + lane);
+                    uint32_t b0 = src_byte(j, mp + lane), b1 = src_byte(j, mp + 64 + lane);
                     uint64_t n0 = __ballot(a0 != b0), n1 = __ballot(a1 != b1);
                     int64_t g = n0 ? __builtin_ctzll(n0) : (n1 ? 64 + __builtin_ctzll(n1) : 128);
                     int64_t l2 = matchlimit - p;
@@ -343,7 +349,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
         CPROF(3);
         int64_t mcode = e - i - 4;
         int64_t lit = i - anchor;
-        op = emit_literals<RING>(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range, rg);
+        op = emit_literals(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range);
         if (range) return op - j.dst_pos;
         uint32_t off = (uint32_t)(i - cand);
         if (lane == 0) { put_byte(j, op, off & 255); put_byte(j, op + 1, (off >> 8) & 255); }
@@ -363,7 +369,7 @@ __device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, b
     if (lane == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
 #endif
-    op = emit_literals<RING>(j, lane, op, anchor, end - anchor, 0, range, rg);
+    op = emit_literals(j, lane, op, anchor, end - anchor, 0, range);
     return op - j.dst_pos;
 }
 
@@ -387,8 +393,7 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
     for (int k = lane; k < 16384; k += kWave) T[k] = j.table ? j.table[k] : 0;
     __syncthreads();
     bool range = false;
-    Ring none{0, 0};
-    int64_t n = compress_block_wave<false>(j, T, lane, range, &none);
+    int64_t n = compress_block_wave(j, T, lane, range);
     __syncthreads();
     if (j.table)
         for (int k = lane; k < 16384; k += kWave) j.table[k] = T[k];
@@ -485,13 +490,14 @@ __device__ __forceinline__ void ring_len_ext(SH& F, FastOut& o, int lane, int64_
 }
 
 // src[pos, pos+n) -> output at op
-template <class SH>
-__device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n) {
+template <class SH, class SRC = SrcG>
+__device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n,
+                          const Ring* rg = nullptr) {
     if (n > kDirectLit) {
         // head into the ring up to a 16-byte boundary, flush, bulk direct, tail into the ring
         const int64_t h = (16 - (o.op & 15)) & 15;
         ring_reserve(F, o, lane, 16);
-        if (lane < h) F.ring[(o.op + lane) & kRingMask] = (uint8_t)src_byte(j, pos + lane);
+        if (lane < h) F.ring[(o.op + lane) & kRingMask] = (uint8_t)SRC::byte(j, rg, pos + lane);
         o.op += h; pos += h; n -= h;
         ring_flush(F, o, lane);
         const int64_t m = n & ~(int64_t)15;
@@ -521,17 +527,17 @@ __device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t
         o.flushed = o.op;
     }
     ring_reserve(F, o, lane, n);
-    for (int64_t t = lane; t < n; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)src_byte(j, pos + t);
+    for (int64_t t = lane; t < n; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)SRC::byte(j, rg, pos + t);
     o.op += n;
 }
 
 // token + literal length + literals
-template <class SH>
+template <class SH, class SRC = SrcG>
 __device__ void fast_literals(SH& F, FastOut& o, const CompJob& j, int lane, int64_t anchor, int64_t lit,
-                              uint32_t mnib) {
+                              uint32_t mnib, const Ring* rg = nullptr) {
     ring_put(F, o, lane, (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib);
     if (lit >= 15) ring_len_ext(F, o, lane, lit - 15);
-    if (lit) ring_copy(F, o, j, lane, anchor, lit);
+    if (lit) ring_copy<SH, SRC>(F, o, j, lane, anchor, lit, rg);
 }
 
 __device__ __forceinline__ uint32_t code_of(const FastShared& F, uint32_t h) {
@@ -559,9 +565,9 @@ __device__ __forceinline__ int64_t skip_sum(uint32_t x) {
 // One sequence's bytes: token, literal length, literals, offset, match length.
 // Common case (at most 14 literals, match length field of at most one extra
 // byte) written by one ds_write_b8 per lane.
-template <class SH>
+template <class SH, class SRC = SrcG>
 __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, int lane, int32_t anchor,
-                                         int32_t pm, uint32_t off, int32_t mcode) {
+                                         int32_t pm, uint32_t off, int32_t mcode, const Ring* rg = nullptr) {
     const int32_t lit = pm - anchor;
     const uint32_t mnib = mcode >= 15 ? 15u : (uint32_t)mcode;
     if (lit < 15 && mcode < 15 + 255) {
@@ -570,7 +576,7 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
         if (lane < total) {
             uint32_t v;
             if (lane == 0) v = ((uint32_t)lit << 4) | mnib;
-            else if (lane <= lit) v = src_byte(j, anchor + lane - 1);
+            else if (lane <= lit) v = SRC::byte(j, rg, anchor + lane - 1);
             else if (lane == lit + 1) v = off & 255;
             else if (lane == lit + 2) v = (off >> 8) & 255;
             else v = (uint32_t)(mcode - 15);
@@ -579,7 +585,7 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
         o.op += total;
         return;
     }
-    fast_literals(F, o, j, lane, anchor, lit, mnib);
+    fast_literals<SH, SRC>(F, o, j, lane, anchor, lit, mnib, rg);
     ring_put(F, o, lane, off & 255);
     ring_put(F, o, lane, (off >> 8) & 255);
     if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
@@ -1000,10 +1006,178 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, in
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
+// ---------------------------------------------------------------------------
 // Dependent blocks (the reference's LZ4.compress default, bufferCompress.js:182-236): the
-// blocks of one frame in order, one hash table carried from block to block (the caller's,
-// in and out), every block's output in its own slot. One wave walks the whole chain; the
-// table (64 KiB) and the source ring (96 KiB) fill the CU's LDS.
+// blocks of one frame in order with one hash table carried from block to block (the
+// caller's Int32Array(16384), in and out: values = absolute position + 1, <= 0 empty), each
+// block's output in its own slot. One wave walks the whole chain, so everything it touches
+// is in LDS: the table (64 KiB, int32 as the reference's), the last 64 KiB of source plus up
+// to 24 KiB ahead (the ring above), the output ring; the probes of a miss chain go as one
+// 64-wide batch as in compress_block_gt. A sequence costs LDS round trips only (the batch
+// encoder's two dependent global round trips per sequence, the old single-wave table kernel's
+// one probe per step, are what made dependent frames 0.027 GB/s).
+struct ChainShared {
+    uint8_t ring[kRing];
+    uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
+};
+__shared__ int32_t g_ctab[16384];
+
+__device__ int64_t compress_block_chain(const CompJob& j, ChainShared& F, int lane, Ring& r) {
+    int32_t* T = g_ctab;
+    const int32_t start = j.start, end = j.start + j.len;
+    const int32_t mflimit = end - 12, matchlimit = end - 5;
+    FastOut o{j.dst, 0, 0};
+    int32_t i = start, anchor = start;
+    uint32_t c = 67;
+    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
+    uint32_t wl = 0;
+    bool pv = false;             // the previous match, emitted after the next probe's reads are issued
+    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
+    uint32_t p_off = 0;
+#if LZ4MI_CPROFILE
+    uint64_t cprof[10] = {0};
+    uint64_t cprof_t = wall_clock64();
+#endif
+    while (i < mflimit) {
+        if (r.hi - i < kRingAhead) ring_advance(j, r, lane, i);
+        CPROF(6);
+        // ---- the probe at i: read and replace, then verification + speculative extension window
+        const int64_t off0 = (int64_t)i - wb;   // positions are absolute: up to 2^31
+        uint32_t seq0;
+        if (off0 >= 0 && off0 + 4 <= 4 * kWave) {
+            const int wi = off0 >> 2;
+            seq0 = funnel(__builtin_amdgcn_readlane(wl, wi), __builtin_amdgcn_readlane(wl, wi < kWave - 1 ? wi + 1 : wi),
+                          (uint32_t)(off0 & 3));
+        } else {
+            seq0 = uniform(SrcR::u32(j, &r, i));
+        }
+        const uint32_t h0 = (seq0 * kP1) >> 18;
+        const int32_t old = T[h0];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) T[h0] = i + 1;
+        int32_t cand0 = old - 1;
+        if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
+        CPROF(0);
+        CPROF_COUNT(8, 1);
+        uint32_t aw = 0, bw = 0;
+        bool hit0 = false;
+        if (cand0 >= 0) {
+            const uint32_t vw = SrcR::u32(j, &r, cand0);
+            aw = SrcR::u32(j, &r, (int64_t)i + 4 + 4 * lane);
+            bw = SrcR::u32(j, &r, (int64_t)cand0 + 4 + 4 * lane);
+            hit0 = uniform(vw) == seq0;
+        }
+        if (pv) {
+            emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
+            pv = false;
+        }
+        CPROF(1);
+        if (hit0) {
+            CPROF_COUNT(9, 1);
+            c = 67;
+            const int32_t lim = matchlimit - (i + 4);
+            const uint32_t x = aw ^ bw;
+            const uint64_t xm = __ballot(x != 0);
+            int32_t f;
+            if (xm) {
+                const int fl = __builtin_ctzll(xm);
+                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
+            } else {
+                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, i + 4 + 4 * kWave,
+                                                                        cand0 + 4 + 4 * kWave, lim - 4 * kWave)
+                                    : lim;
+            }
+            if (f > lim) f = lim;
+            wb = i + 4;
+            wl = aw;
+            const int32_t e = i + 4 + f;
+            pv = true;
+            p_anchor = anchor;
+            p_pm = i;
+            p_off = (uint32_t)(i - cand0);
+            p_mcode = e - i - 4;
+            i = e;
+            anchor = e;
+            CPROF(3);
+            continue;
+        }
+        // ---- the probe at i missed (and inserted itself): the next probes of the miss chain as a batch
+        i += (int32_t)(c >> 6);
+        c += 1;
+        if (i >= mflimit) break;
+        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const uint32_t step = (c + lane) >> 6;
+        bool act = p < mflimit;
+        uint32_t seq = 0;
+        {
+            const int64_t off = (int64_t)p - wb;
+            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
+            const int wi = inw ? (off >> 2) : 0;
+            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
+            seq = funnel(w0, w1, (uint32_t)(off & 3));
+            if (__ballot(act && !inw)) {
+                if (act && !inw) seq = SrcR::u32(j, &r, p);
+            }
+        }
+        const uint32_t h = (seq * kP1) >> 18;
+        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
+            volatile uint8_t* vs = F.slot;
+            if (act) vs[h & 1023] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool dup = act && vs[h & 1023] != (uint8_t)lane;
+            int nb = __popcll(__ballot(act));
+            const uint64_t dm = __ballot(dup);
+            if (dm) {
+                const int d = __builtin_ctzll(dm);
+                nb = d ? d : 1;
+            }
+            act = act && lane < nb;
+        }
+        const int nb = __popcll(__ballot(act));
+        int32_t cand = -1;
+        if (act) {
+            const int32_t ov = T[h];
+            cand = ov - 1;
+            if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
+        }
+        const uint32_t vw = cand >= 0 ? SrcR::u32(j, &r, cand) : 0u;
+        const uint64_t hm = __ballot(cand >= 0 && vw == seq);
+        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
+        __builtin_amdgcn_wave_barrier();
+        CPROF(2);
+        if (!hm) {
+            i = lane_val(p + (int32_t)step, nb - 1);
+            c += nb;
+            continue;
+        }
+        CPROF_COUNT(9, 1);
+        const int m = nprobe - 1;
+        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
+        c = 67;
+        const int32_t e = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
+        pv = true;
+        p_anchor = anchor;
+        p_pm = pm;
+        p_off = (uint32_t)(pm - cm);
+        p_mcode = e - pm - 4;
+        i = e;
+        anchor = e;
+        CPROF(3);
+    }
+    if (pv) emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
+    fast_literals<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, 0, &r);
+    ring_flush(F, o, lane);
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    CPROF(4);
+#if LZ4MI_CPROFILE
+    if (lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
+#endif
+    return o.op;
+}
+
 struct ChainArgs {
     const uint8_t* src;
     uint64_t src_total;
@@ -1016,9 +1190,9 @@ struct ChainArgs {
 };
 
 __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
-    __shared__ int32_t T[16384];
+    __shared__ ChainShared F;
     const int lane = threadIdx.x;
-    for (int k = lane; k < 16384; k += kWave) T[k] = a.table[k];
+    for (int k = lane; k < 16384; k += kWave) g_ctab[k] = a.table[k];
     __syncthreads();
     int64_t lo = (int64_t)a.start - 65536;
     lo = lo < 0 ? 0 : (lo & ~(int64_t)15);
@@ -1029,12 +1203,11 @@ __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
         const int32_t n = (int32_t)(rest < a.bsize ? rest : a.bsize);
         CompJob j{a.src, a.src_total, (int32_t)s0, n, a.out + a.out_off[b],
                   (uint64_t)n + (uint64_t)n / 255u + 16u, 0, nullptr};
-        bool range = false;
-        const int64_t w = compress_block_wave<true>(j, T, lane, range, &r);
+        const int64_t w = compress_block_chain(j, F, lane, r);
         if (lane == 0) a.comp_len[b] = (uint32_t)w;
     }
     __syncthreads();
-    for (int k = lane; k < 16384; k += kWave) a.table[k] = T[k];
+    for (int k = lane; k < 16384; k += kWave) a.table[k] = g_ctab[k];
 }
 
 }  // namespace lz4mi

@@ -17,7 +17,7 @@ L.lz4mi_compress_block_table.restype = ctypes.c_int64
 assert L.lz4mi_init(0) == 0
 buf = (ctypes.c_ulonglong * 16)()
 BS = 4 << 20
-names = ["seq+hash", "table", "cand fetch", "extend", "emit"]
+names = ["head probe", "reads+emit", "batch", "extend", "tail", "", "ring"]
 for gen in (sys.argv[1] if len(sys.argv) > 1 else "tiles216,random").split(","):
     data = O.generate(gen, 7, BS)
     for mode in ("chain", "table"):

@@ -24,4 +24,6 @@ fi
 if has pmc; then
   timeout -k 10 900 bash tools/pmc_traffic.sh gpurun_out/$TAG/pmc tiles216 > gpurun_out/$TAG/pmc.log 2>&1 || { echo pmc failed; tail -5 gpurun_out/$TAG/pmc.log; exit 1; }
   echo "pmc ok"; tail -12 gpurun_out/$TAG/pmc.log
+  timeout -k 10 900 bash tools/pmc_traffic.sh gpurun_out/$TAG/pmc_c tiles216 compress > gpurun_out/$TAG/pmc_c.log 2>&1 || { echo pmc compress failed; tail -5 gpurun_out/$TAG/pmc_c.log; exit 1; }
+  echo "pmc compress ok"; tail -12 gpurun_out/$TAG/pmc_c.log
 fi

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Summarise FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) into the
-bench's roofline.traffic record: HBM-side bytes per decompress launch.
+bench's roofline.traffic record: HBM-side bytes per launch of the decompress
+(default) or compress kernel.
 FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 128-B read
 requests at 64 B, so it is doubled (MI355X_MICROARCH.md, HBM section)."""
 import csv, glob, json, os, sys
@@ -9,18 +10,19 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import lz4mi  # noqa: E402  (build id only: loads the library, no GPU call)
 
 root, gen = sys.argv[1], sys.argv[2]
+kernel = sys.argv[3] if len(sys.argv) > 3 else "lz4mi_decompress_kernel"
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     v = []
     for f in glob.glob(f"{root}/{c}/**/pmc_counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "lz4mi_decompress_kernel" in r["Kernel_Name"] and r["Counter_Name"] == c:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == c:
                 v.append(float(r["Counter_Value"]))
     vals[c] = v
 # the microbench runs the kernel once for warm-up and once timed: take the last dispatch
 fetch = vals["FETCH_SIZE"][-1] * 1024 * 2
 write = vals["WRITE_SIZE"][-1] * 1024
-print(json.dumps({"generator": gen, "workload_blocks": 4096, "kernel": "lz4mi_decompress_kernel",
+print(json.dumps({"generator": gen, "workload_blocks": 4096, "kernel": kernel,
                   "fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
                   "dispatches_seen": {k: len(v) for k, v in vals.items()}, "build_id": lz4mi.build_id(),
                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950), KiB->B"},
