@@ -447,7 +447,7 @@ struct FastOut {
 
 // ring [flushed, floor16(op)) -> dst
 template <class SH>
-__device__ void ring_flush(SH& F, FastOut& o, int lane) {
+__device__ __forceinline__ void ring_flush(SH& F, FastOut& o, int lane) {
     const int64_t upto = o.op & ~(int64_t)15;
     for (int64_t p = o.flushed + 16 * lane; p < upto; p += 16 * kWave) {
         uint4 v;
@@ -562,12 +562,37 @@ __device__ __forceinline__ int64_t skip_sum(uint32_t x) {
     return 32 * q * (q - 1) + r * q;
 }
 
+// The general case of emit_seq (15+ literals or a match length field of 2+ extra bytes),
+// out of line with the output state passed by value and returned: inlining it at every
+// emission site costs the batch encoders their registers, and a FastOut passed by reference
+// to a call lives in scratch memory (every emission then reads it back with a vmcnt(0) wait).
+template <class SH, class SRC = SrcG>
+__device__ __noinline__ FastOut emit_general(SH& F, FastOut o, const CompJob& j, int lane, int32_t anchor, int32_t pm,
+                                             uint32_t off, int32_t mcode, const Ring* rg) {
+    const int32_t lit = pm - anchor;
+    const uint32_t mnib = mcode >= 15 ? 15u : (uint32_t)mcode;
+    fast_literals<SH, SRC>(F, o, j, lane, anchor, lit, mnib, rg);
+    ring_put(F, o, lane, off & 255);
+    ring_put(F, o, lane, (off >> 8) & 255);
+    if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
+    return o;
+}
+
+// The final literal run (out of line, as emit_general).
+template <class SH, class SRC = SrcG>
+__device__ __noinline__ FastOut emit_tail(SH& F, FastOut o, const CompJob& j, int lane, int64_t anchor, int64_t lit,
+                                          const Ring* rg) {
+    fast_literals<SH, SRC>(F, o, j, lane, anchor, lit, 0, rg);
+    return o;
+}
+
 // One sequence's bytes: token, literal length, literals, offset, match length.
 // Common case (at most 14 literals, match length field of at most one extra
 // byte) written by one ds_write_b8 per lane.
 template <class SH, class SRC = SrcG>
 __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, int lane, int32_t anchor,
-                                         int32_t pm, uint32_t off, int32_t mcode, const Ring* rg = nullptr) {
+                                         int32_t pm, uint32_t off, int32_t mcode, const Ring* rg = nullptr,
+                                         bool has_pre = false, uint32_t pre = 0) {
     const int32_t lit = pm - anchor;
     const uint32_t mnib = mcode >= 15 ? 15u : (uint32_t)mcode;
     if (lit < 15 && mcode < 15 + 255) {
@@ -576,7 +601,7 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
         if (lane < total) {
             uint32_t v;
             if (lane == 0) v = ((uint32_t)lit << 4) | mnib;
-            else if (lane <= lit) v = SRC::byte(j, rg, anchor + lane - 1);
+            else if (lane <= lit) v = has_pre ? pre : SRC::byte(j, rg, anchor + lane - 1);   // pre: loaded earlier
             else if (lane == lit + 1) v = off & 255;
             else if (lane == lit + 2) v = (off >> 8) & 255;
             else v = (uint32_t)(mcode - 15);
@@ -585,10 +610,7 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
         o.op += total;
         return;
     }
-    fast_literals<SH, SRC>(F, o, j, lane, anchor, lit, mnib, rg);
-    ring_put(F, o, lane, off & 255);
-    ring_put(F, o, lane, (off >> 8) & 255);
-    if (mcode >= 15) ring_len_ext(F, o, lane, mcode - 15);
+    o = emit_general<SH, SRC>(F, o, j, lane, anchor, pm, off, mcode, rg);
 }
 
 __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane) {
@@ -729,7 +751,7 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
     if (lane == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
 #endif
-    fast_literals(F, o, j, lane, anchor, n - anchor, 0);
+    o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
     for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
     return o.op;
@@ -983,10 +1005,330 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
         anchor = e;
     }
     if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-    fast_literals(F, o, j, lane, anchor, n - anchor, 0);
+    o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
     for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
     return o.op;
+}
+
+// ---------------------------------------------------------------------------
+// Speculative hit chains (round 3, default). After a hit of step S (match end -
+// probe position) the next probe is at the match end, and on mid-ratio data the
+// next match often has the same step again (tiles216: 94 % of matches are 64
+// bytes and followed directly by a hit). compress_block_gt spends two dependent
+// global round trips per sequence (table, then the candidate's bytes); here one
+// batch probes up to kSpecK positions i, i + S, i + 2S, ... at once, assuming each
+// is a hit of step S:
+//   round 1: the K table reads (a probe whose hash repeats an earlier probe of the
+//            batch takes that probe's position instead: it inserts first);
+//   round 2: per probe, 128 bytes at the probe and at its candidate (8 lanes x 16
+//            bytes; the first differing byte is the match length when < 128), and
+//            the 4 bytes at each probe position of the next batch (prefetch);
+// then the probes are accepted in order while each is a hit whose end is the next
+// probe's position. Every accepted probe and the first rejected one (the probe at
+// the end of the last accepted match, which does happen) are exactly the serial
+// parse's probes: they insert their positions (the last of equal hashes wins), and
+// the parse continues from there -- the next batch, or the miss chain on a miss.
+// Round trips per sequence: 2 / (accepted probes per batch); tiles216 3.8 (CPU model
+// of the serial parse, K = 8). Table reads after the previous batch's stores need no
+// wait: one wave's load of an address it stored to observes the store (program order).
+#ifndef LZ4MI_GTSPEC
+#define LZ4MI_GTSPEC 1
+#endif
+constexpr int kSpecK = 8;     // probes per speculative batch (8 lanes each for the windows)
+constexpr int kSpecW = 128;   // window bytes per probe
+
+// 16 source bytes at p (zero past the end).
+__device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
+    uint4 v;
+    if (p >= 0 && (uint64_t)p + 16 <= j.src_total) {
+        __builtin_memcpy(&v, j.src + p, 16);
+        return v;
+    }
+    return make_uint4(ld_u32(j, p), ld_u32(j, p + 4), ld_u32(j, p + 8), ld_u32(j, p + 12));
+}
+
+// Index of the first nonzero byte of x (16 if none).
+__device__ __forceinline__ uint32_t first_nz16(uint4 x) {
+    return x.x ? (__builtin_ctz(x.x) >> 3)
+               : x.y ? 4 + (__builtin_ctz(x.y) >> 3)
+                     : x.z ? 8 + (__builtin_ctz(x.z) >> 3) : x.w ? 12 + (__builtin_ctz(x.w) >> 3) : 16u;
+}
+
+// 4 bytes at offset o (0 <= o <= kSpecW - 4) of a 128-byte window held as uint4s by
+// lanes l0 .. l0 + 7 (o per lane).
+__device__ __forceinline__ uint32_t win_u32(const uint4& wv, int l0, int32_t o) {
+    const int q = o >> 2, L = l0 + (q >> 2), r = q & 3;
+    const uint32_t x0 = __shfl(wv.x, L, kWave), x1 = __shfl(wv.y, L, kWave), x2 = __shfl(wv.z, L, kWave),
+                   x3 = __shfl(wv.w, L, kWave), nx = __shfl(wv.x, L < kWave - 1 ? L + 1 : L, kWave);
+    const uint32_t d0 = r == 0 ? x0 : r == 1 ? x1 : r == 2 ? x2 : x3;
+    const uint32_t d1 = r == 0 ? x1 : r == 1 ? x2 : r == 2 ? x3 : nx;
+    return funnel(d0, d1, (uint32_t)(o & 3));
+}
+
+__device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T, int lane) {
+    const int32_t n = j.len;
+    const int32_t mflimit = n - 12, matchlimit = n - 5;
+    FastOut o{j.dst, 0, 0};
+    int32_t i = 0, anchor = 0;
+    uint32_t c = 67;
+    int32_t S = 0;                       // step of the last hit (0: none): the speculated distance between probes
+    // accepted sequences not emitted yet (lanes 0 .. npend-1: probe, candidate, match end),
+    // emitted while the next batch's table reads are in flight
+    int npend = 0;
+    int32_t pd_p = 0, pd_c = 0, pd_e = 0;
+    int32_t pf_pos = -1;                 // lanes < kSpecK: 4 source bytes at pf_pos, loaded ahead
+    uint32_t pf_seq = 0;
+    int32_t wbase = -(1 << 30);          // 128-byte source window [wbase, wbase + 128) in lanes wl0 .. wl0 + 7
+    int wl0 = 0;
+    uint4 wv = make_uint4(0, 0, 0, 0);
+    uint16_t* T16 = (uint16_t*)T;
+    int32_t g = 0;
+    for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
+    for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
+    wait_vmem();
+#if LZ4MI_CPROFILE
+    uint64_t cprof[16] = {0};
+    uint64_t cprof_t = wall_clock64();
+#endif
+    // Only the first pending sequence can have literals (the others are back-to-back hits).
+    // Its 1..14 literal bytes (lane l: byte l - 1) are loaded and waited for before the
+    // emission, so no load is pending inside it but the next batch's table reads: the inline
+    // emission never waits for memory (longer runs go through emit_general, out of line).
+    auto load_lit = [&]() -> uint32_t {
+        uint32_t litv = 0;
+        const int32_t lit0 = lane_val(pd_p, 0) - anchor;
+        const bool ld = lit0 > 0 && lit0 < 15 && lane >= 1 && lane <= lit0;
+        if (__ballot(ld)) {
+            if (ld) litv = src_byte(j, anchor + lane - 1);
+            wait_vmem();
+        }
+        settle32(litv);
+        return litv;
+    };
+    auto emit_pending = [&](uint32_t litv) {
+        for (int k = 0; k < npend; ++k) {
+            const int32_t pm = lane_val(pd_p, k), cm = lane_val(pd_c, k), e = lane_val(pd_e, k);
+            emit_seq(F, o, j, lane, anchor, pm, (uint32_t)(pm - cm), e - pm - 4, nullptr, true, litv);
+            anchor = e;
+        }
+        npend = 0;
+    };
+    auto insert = [&](bool ins, uint32_t h, int32_t p) {   // distinct hashes among inserting lanes
+        if (ins) {
+            T16[h] = (uint16_t)(p & 0x7FFF);
+            const uint32_t sh = (h & 15) * 2;                  // two hashes may share a code word: LDS atomics
+            atomicAnd(&F.code[h >> 4], ~(3u << sh));
+            atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
+        }
+    };
+    while (i < mflimit) {
+        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+        __builtin_amdgcn_s_setprio(3);
+        // ---- the batch: probes at i + kS, k < K, each assumed a hit of step S
+        int K = 1;
+        if (c == 67 && S > 0) {
+            const int32_t lim = min(mflimit - 1, ((g + 1) << 15) - 1) - i;   // same epoch, before mflimit
+            K = 1 + lim / S;
+            if (K > kSpecK) K = kSpecK;
+        }
+        const bool act = lane < K;
+        const int32_t p = i + lane * S;
+        uint32_t seq = pf_seq;
+        {
+            const int32_t ow = p - wbase;
+            const bool inw = ow >= 0 && ow + 4 <= kSpecW;
+            const uint32_t ws = win_u32(wv, wl0, inw ? ow : 0);
+            if (inw) seq = ws;
+            if (__ballot(act && !inw && pf_pos != p)) {
+                if (act && !inw && pf_pos != p) seq = ld_u32(j, p);
+            }
+        }
+        const uint32_t h = (seq * kP1) >> 18;
+        int32_t cand = -1;
+        bool dup = false;
+        for (int k = 0; k + 1 < K; ++k) {                       // an earlier probe of the batch with this hash
+            if (lane > k && lane_val(h, k) == h) {
+                cand = i + k * S;
+                dup = true;
+            }
+        }
+        const uint32_t litv = npend ? load_lit() : 0u;
+        CPROF(0);
+        CPROF_COUNT(8, 1);
+        uint32_t tlo = 0, tcd = 0;
+        if (act && !dup) {
+            tlo = T16[h];
+            tcd = gt_code_of(F, h);
+        }
+        if (npend) {                                            // off the chain, while the reads are in flight
+            __builtin_amdgcn_s_setprio(0);
+            emit_pending(litv);
+            __builtin_amdgcn_s_setprio(3);
+        }
+        // (the read's value is opaque until here: otherwise the compiler consumes it, and
+        // waits for it, right after the load, before the emission)
+        asm volatile("" : "+v"(tlo) :: "memory");
+        CPROF(1);
+        if (act && !dup) cand = gt16_decode(tlo, tcd, g);
+        if (cand >= 0 && (p - cand < 1 || p - cand > 65535)) cand = -1;
+        // ---- windows: lanes 8k .. 8k+7 hold 128 bytes at probe k and at its candidate
+        const int gk = lane >> 3, gt = lane & 7;
+        const int32_t gc = __shfl(cand, gk, kWave);
+        uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
+        if (gk < K) {
+            xa = ld16(j, (int64_t)i + gk * S + 16 * gt);
+            if (gc >= 0) xb = ld16(j, (int64_t)gc + 16 * gt);
+        }
+        {   // the next batch's probe bytes, assuming all K probes hit with step S
+            const int32_t q = i + (K + lane) * S;
+            pf_pos = (c == 67 && S > 0 && lane < kSpecK && q < mflimit) ? q : -1;
+            if (pf_pos >= 0) pf_seq = ld_u32(j, pf_pos);
+        }
+        CPROF(2);
+        wait_vmem();              // the windows and the prefetch (issued together): later uses never wait
+        settle32(pf_seq);
+        settle32(xa.x);
+        settle32(xa.y);
+        settle32(xa.z);
+        settle32(xa.w);
+        settle32(xb.x);
+        settle32(xb.y);
+        settle32(xb.z);
+        settle32(xb.w);
+        const uint32_t lm = (gk < K && gc >= 0) ? first_nz16(make_uint4(xa.x ^ xb.x, xa.y ^ xb.y, xa.z ^ xb.z, xa.w ^ xb.w))
+                                                : 0u;
+        const uint64_t mm = __ballot(lm < 16);
+        // lane k < K: bytes equal at probe k (m, 128 = the whole window)
+        const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
+        const int ft = gm ? __builtin_ctz(gm) : 0;
+        const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
+        const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
+        const bool hit = act && cand >= 0 && m >= 4;
+        const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;
+        const int32_t e = p + (m < matchlimit - p ? m : matchlimit - p);
+        const bool ok = hit && !lng && lane + 1 < K && e == p + S;
+        const int J = __builtin_ctzll(__ballot(act && !ok));   // the first probe that ends the batch
+        CPROF(3);
+        CPROF_COUNT(9, J);
+        // probes 0 .. J happened: each inserts its position (the last of equal hashes)
+        bool later = false;
+        for (int k = 1; k <= J; ++k)
+            if (k > lane && lane_val(h, k) == h) later = true;
+        insert(lane <= J && !later, h, p);
+        wbase = i + J * S;                                      // the miss chain reads its bytes from probe J's window
+        wl0 = 8 * J;
+        wv = xa;
+        const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
+        const bool hitJ = (__ballot(hit) >> J) & 1ull;
+        pd_p = p;
+        pd_c = cand;
+        pd_e = e;
+        CPROF(4);
+        if (hitJ) {
+            CPROF_COUNT(9, 1);
+            int32_t eJ = lane_val(e, J);
+            if ((__ballot(lng) >> J) & 1ull)
+                eJ = pJ + kSpecW + (int32_t)match_extent(j, lane, pJ + kSpecW, cJ + kSpecW, matchlimit - (pJ + kSpecW));
+            if (lane == J) pd_e = eJ;
+            npend = J + 1;
+            c = 67;                                             // (a single probe after a miss chain may hit)
+            CPROF(5);
+            S = eJ - pJ;
+            i = eJ;
+            continue;
+        }
+        // ---- probe J missed (and inserted itself): the accepted hits go out, then the
+        // next probes of the miss chain as a batch
+        CPROF_COUNT(10, 1);
+        npend = J;
+        if (npend) emit_pending(load_lit());
+        CPROF(6);
+        i = pJ + (int32_t)(c >> 6);
+        c += 1;
+        if (i >= mflimit) break;
+        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+        const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const uint32_t step = (c + lane) >> 6;
+        bool mact = pm_ < mflimit && (pm_ >> 15) == g;          // probes of the next epoch: the next batch
+        uint32_t mseq = 0;
+        {
+            const int32_t ow = pm_ - wbase;
+            const bool inw = ow >= 0 && ow + 4 <= kSpecW;
+            mseq = win_u32(wv, wl0, inw ? ow : 0);
+            if (__ballot(mact && !inw)) {
+                if (mact && !inw) mseq = ld_u32(j, pm_);
+            }
+        }
+        const uint32_t mh = (mseq * kP1) >> 18;
+        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
+            volatile uint8_t* vs = F.slot;
+            if (mact) vs[mh & 1023] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool mdup = mact && vs[mh & 1023] != (uint8_t)lane;
+            int nb = __popcll(__ballot(mact));
+            const uint64_t dm = __ballot(mdup);
+            if (dm) {
+                const int d = __builtin_ctzll(dm);
+                nb = d ? d : 1;
+            }
+            mact = mact && lane < nb;
+        }
+        const int nb = __popcll(__ballot(mact));
+        int32_t mc = -1;
+        if (mact) {
+            mc = gt16_decode(T16[mh], gt_code_of(F, mh), g);
+            if (mc < 0 || pm_ - mc < 1 || pm_ - mc > 65535) mc = -1;
+        }
+        const uint32_t vw = mc >= 0 ? ld_u32(j, mc) : 0u;
+        const uint64_t hm = __ballot(mc >= 0 && vw == mseq);
+        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+        insert(lane < nprobe, mh, pm_);                         // the probes that happen
+        if (!hm) {
+            i = lane_val(pm_ + (int32_t)step, nb - 1);
+            c += nb;
+            S = 0;
+            CPROF(7);
+            continue;
+        }
+        const int mi = nprobe - 1;
+        const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
+        c = 67;
+        const int32_t e1 = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
+        pd_p = pm;
+        pd_c = cm;
+        pd_e = e1;
+        npend = 1;
+        S = e1 - pm;
+        i = e1;
+        CPROF(7);
+    }
+#if LZ4MI_CPROFILE
+    if (lane == 0)
+        for (int k = 0; k < 12; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
+#endif
+    if (npend) emit_pending(load_lit());
+    o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
+    ring_flush(F, o, lane);
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    return o.op;
+}
+
+__global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, int32_t* tables) {
+    __shared__ GtShared F;
+    const uint32_t b = blockIdx.x;
+    if (b >= a.nblocks) return;
+    CompJob j;
+    j.src = a.in + a.in_off[b];
+    j.src_total = a.in_len[b];
+    j.start = 0;
+    j.len = (int32_t)a.in_len[b];
+    j.dst = a.out + a.out_off[b];
+    j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
+    j.dst_pos = 0;
+    j.table = nullptr;
+    const int64_t r = compress_block_gts(j, F, tables + (size_t)b * 16384, threadIdx.x);
+    if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
 __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, int32_t* tables) {
@@ -1167,7 +1509,7 @@ __device__ int64_t compress_block_chain(const CompJob& j, ChainShared& F, int la
         CPROF(3);
     }
     if (pv) emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
-    fast_literals<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, 0, &r);
+    o = emit_tail<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, &r);
     ring_flush(F, o, lane);
     for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
     CPROF(4);
@@ -1234,7 +1576,12 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
         hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
+    // LZ4MI_ENCODER=gt: the one-sequence-per-round-trip batch encoder (A/B against the default)
+    if (!LZ4MI_GTSPEC || (enc && enc[0] == 'g')) {
+        hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
     return hipGetLastError();
 }
 
