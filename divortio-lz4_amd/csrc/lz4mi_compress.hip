@@ -431,6 +431,8 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
 constexpr int kCodeWords = 16384 / 16;
 constexpr int kRing = 4096;
 constexpr int kRingMask = kRing - 1;
+#define RING_SZ(F) ((int64_t)sizeof((F).ring))   // the output ring's size in the caller's shared struct
+#define RING_MASK(F) (RING_SZ(F) - 1)
 constexpr int32_t kDirectLit = 2048;   // longer literal runs bypass the ring
 
 struct FastShared {
@@ -451,7 +453,7 @@ __device__ __forceinline__ void ring_flush(SH& F, FastOut& o, int lane) {
     const int64_t upto = o.op & ~(int64_t)15;
     for (int64_t p = o.flushed + 16 * lane; p < upto; p += 16 * kWave) {
         uint4 v;
-        __builtin_memcpy(&v, F.ring + (p & kRingMask), 16);
+        __builtin_memcpy(&v, F.ring + (p & RING_MASK(F)), 16);
         __builtin_memcpy(o.dst + p, &v, 16);
     }
     if (upto > o.flushed) o.flushed = upto;
@@ -459,16 +461,16 @@ __device__ __forceinline__ void ring_flush(SH& F, FastOut& o, int lane) {
 
 template <class SH>
 __device__ __forceinline__ void ring_reserve(SH& F, FastOut& o, int lane, int64_t n) {
-    if (o.op + n - o.flushed > kRing) ring_flush(F, o, lane);
+    if (o.op + n - o.flushed > RING_SZ(F)) ring_flush(F, o, lane);
 }
 
-// n bytes of value v (n <= kRing - 16 per call)
+// n bytes of value v (n <= RING_SZ(F) - 16 per call)
 template <class SH>
 __device__ void ring_fill(SH& F, FastOut& o, int lane, int64_t n, uint32_t v) {
     while (n > 0) {
-        const int64_t k = n < kRing - 16 ? n : kRing - 16;
+        const int64_t k = n < RING_SZ(F) - 16 ? n : RING_SZ(F) - 16;
         ring_reserve(F, o, lane, k);
-        for (int64_t t = lane; t < k; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)v;
+        for (int64_t t = lane; t < k; t += kWave) F.ring[(o.op + t) & RING_MASK(F)] = (uint8_t)v;
         o.op += k;
         n -= k;
     }
@@ -477,7 +479,7 @@ __device__ void ring_fill(SH& F, FastOut& o, int lane, int64_t n, uint32_t v) {
 template <class SH>
 __device__ __forceinline__ void ring_put(SH& F, FastOut& o, int lane, uint32_t v) {
     ring_reserve(F, o, lane, 1);
-    if (lane == 0) F.ring[o.op & kRingMask] = (uint8_t)v;
+    if (lane == 0) F.ring[o.op & RING_MASK(F)] = (uint8_t)v;
     o.op += 1;
 }
 
@@ -497,7 +499,7 @@ __device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t
         // head into the ring up to a 16-byte boundary, flush, bulk direct, tail into the ring
         const int64_t h = (16 - (o.op & 15)) & 15;
         ring_reserve(F, o, lane, 16);
-        if (lane < h) F.ring[(o.op + lane) & kRingMask] = (uint8_t)SRC::byte(j, rg, pos + lane);
+        if (lane < h) F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)SRC::byte(j, rg, pos + lane);
         o.op += h; pos += h; n -= h;
         ring_flush(F, o, lane);
         const int64_t m = n & ~(int64_t)15;
@@ -527,7 +529,7 @@ __device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t
         o.flushed = o.op;
     }
     ring_reserve(F, o, lane, n);
-    for (int64_t t = lane; t < n; t += kWave) F.ring[(o.op + t) & kRingMask] = (uint8_t)SRC::byte(j, rg, pos + t);
+    for (int64_t t = lane; t < n; t += kWave) F.ring[(o.op + t) & RING_MASK(F)] = (uint8_t)SRC::byte(j, rg, pos + t);
     o.op += n;
 }
 
@@ -605,7 +607,7 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
             else if (lane == lit + 1) v = off & 255;
             else if (lane == lit + 2) v = (off >> 8) & 255;
             else v = (uint32_t)(mcode - 15);
-            F.ring[(o.op + lane) & kRingMask] = (uint8_t)v;
+            F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
         }
         o.op += total;
         return;
@@ -753,7 +755,7 @@ __device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane
 #endif
     o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
     return o.op;
 }
 
@@ -804,10 +806,12 @@ __device__ __forceinline__ int32_t gt16_decode(uint32_t lo, uint32_t cd, int32_t
     const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
     return ge < 0 ? -1 : ((ge << 15) | (int32_t)(lo & 0x7FFFu));
 }
-__device__ __forceinline__ uint32_t gt_code_of(const GtShared& F, uint32_t h) {
+template <class SH>
+__device__ __forceinline__ uint32_t gt_code_of(const SH& F, uint32_t h) {
     return (F.code[h >> 4] >> ((h & 15) * 2)) & 3u;
 }
-__device__ void gt_scrub_epoch(GtShared& F, int lane, int32_t g) {
+template <class SH>
+__device__ void gt_scrub_epoch(SH& F, int lane, int32_t g) {
     const uint32_t X = (uint32_t)(g & 3) * 0x55555555u, Y = (uint32_t)((g + 1) & 3) * 0x55555555u;
     for (int w = lane; w < kCodeWords; w += kWave) {
         const uint32_t v = F.code[w], x = v ^ X;
@@ -1007,7 +1011,7 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
     if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
     o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
     return o.op;
 }
 
@@ -1055,33 +1059,27 @@ __device__ __forceinline__ uint32_t first_nz16(uint4 x) {
                      : x.z ? 8 + (__builtin_ctz(x.z) >> 3) : x.w ? 12 + (__builtin_ctz(x.w) >> 3) : 16u;
 }
 
-// 4 bytes at offset o (0 <= o <= kSpecW - 4) of a 128-byte window held as uint4s by
-// lanes l0 .. l0 + 7 (o per lane).
-__device__ __forceinline__ uint32_t win_u32(const uint4& wv, int l0, int32_t o) {
-    const int q = o >> 2, L = l0 + (q >> 2), r = q & 3;
-    const uint32_t x0 = __shfl(wv.x, L, kWave), x1 = __shfl(wv.y, L, kWave), x2 = __shfl(wv.z, L, kWave),
-                   x3 = __shfl(wv.w, L, kWave), nx = __shfl(wv.x, L < kWave - 1 ? L + 1 : L, kWave);
-    const uint32_t d0 = r == 0 ? x0 : r == 1 ? x1 : r == 2 ? x2 : x3;
-    const uint32_t d1 = r == 0 ? x1 : r == 1 ? x2 : r == 2 ? x3 : nx;
-    return funnel(d0, d1, (uint32_t)(o & 3));
-}
+constexpr int32_t kWinBytes = 2048;   // source window in LDS: the probes' 4-byte reads
 
-__device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T, int lane) {
+struct GtsShared {
+    uint8_t ring[2048];                  // output ring (half the batch encoder's: the window takes the rest)
+    uint8_t slot[1024];                  // miss batches: lane ids keyed by hash & 1023
+    uint32_t code[kCodeWords];           // 2-bit epoch code per table entry
+    uint32_t win[kWinBytes / 4 + 4];     // source bytes [wb, wb + kWinBytes)
+};
+
+__device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T, int lane) {
     const int32_t n = j.len;
     const int32_t mflimit = n - 12, matchlimit = n - 5;
     FastOut o{j.dst, 0, 0};
     int32_t i = 0, anchor = 0;
     uint32_t c = 67;
-    int32_t S = 0;                       // step of the last hit (0: none): the speculated distance between probes
+    int32_t S = 0;                       // step of the last hit (0: in a miss chain): the speculated probe distance
     // accepted sequences not emitted yet (lanes 0 .. npend-1: probe, candidate, match end),
     // emitted while the next batch's table reads are in flight
     int npend = 0;
     int32_t pd_p = 0, pd_c = 0, pd_e = 0;
-    int32_t pf_pos = -1;                 // lanes < kSpecK: 4 source bytes at pf_pos, loaded ahead
-    uint32_t pf_seq = 0;
-    int32_t wbase = -(1 << 30);          // 128-byte source window [wbase, wbase + 128) in lanes wl0 .. wl0 + 7
-    int wl0 = 0;
-    uint4 wv = make_uint4(0, 0, 0, 0);
+    int32_t wb = -(1 << 30);             // F.win holds source [wb, wb + kWinBytes)
     uint16_t* T16 = (uint16_t*)T;
     int32_t g = 0;
     for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
@@ -1099,7 +1097,11 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T,
         uint32_t litv = 0;
         const int32_t lit0 = lane_val(pd_p, 0) - anchor;
         const bool ld = lit0 > 0 && lit0 < 15 && lane >= 1 && lane <= lit0;
-        if (__ballot(ld)) {
+        const int32_t ow = anchor - wb;
+        if (ow >= 0 && ow + lit0 + 4 <= kWinBytes) {          // from the window
+            const int32_t q = ow + lane - 1;
+            if (ld) litv = (F.win[q >> 2] >> (8 * (q & 3))) & 255u;
+        } else if (__ballot(ld)) {
             if (ld) litv = src_byte(j, anchor + lane - 1);
             wait_vmem();
         }
@@ -1114,6 +1116,54 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T,
         }
         npend = 0;
     };
+    // All pending sequences in one ring write when each is the common case (sequence 0 has
+    // < 15 literals, every match length field at most one extra byte): lane k < npend has
+    // size_k = token + literals + offset + extension bytes at ring offset start_k; output
+    // lane t finds its sequence among the <= 8 starts. Else one sequence at a time.
+    auto emit_batch = [&](uint32_t litv) {
+        const int32_t lit0 = lane_val(pd_p, 0) - anchor;
+        const int32_t mcode = pd_e - pd_p - 4;
+        const bool mine = lane < npend;
+        if (lit0 >= 15 || __ballot(mine && mcode >= 15 + 255)) {
+            emit_pending(litv);
+            return;
+        }
+        const int32_t lit = lane == 0 ? lit0 : 0;
+        const uint32_t size = mine ? 3u + (uint32_t)lit + (mcode >= 15 ? 1u : 0u) : 0u;
+        uint32_t incl = size;                                   // inclusive scan over lanes 0..7 (row 0)
+        incl += dpp<kRowShr1>(0u, incl);
+        incl += dpp<kRowShr2>(0u, incl);
+        incl += dpp<kRowShr4>(0u, incl);
+        const uint32_t start = incl - size;
+        const int32_t total = (int32_t)lane_val(incl, npend - 1);
+        const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
+        const uint32_t off = (uint32_t)(pd_p - pd_c);
+        ring_reserve(F, o, lane, total);
+        int32_t r = lane, cl = 0;
+        uint32_t ct = 0, co = 0, cm = 0;
+        for (int k = 0; k < npend; ++k) {
+            const int32_t sk = (int32_t)lane_val(start, k);
+            if (lane >= sk) {
+                r = lane - sk;
+                cl = k == 0 ? lit0 : 0;
+                ct = lane_val(tok, k);
+                co = lane_val(off, k);
+                cm = (uint32_t)lane_val(mcode, k);
+            }
+        }
+        if (lane < total) {
+            uint32_t v;
+            if (r == 0) v = ct;
+            else if (r <= cl) v = litv;                         // sequence 0 starts at 0: lane r holds byte r - 1
+            else if (r == cl + 1) v = co & 255;
+            else if (r == cl + 2) v = (co >> 8) & 255;
+            else v = cm - 15;
+            F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
+        }
+        o.op += total;
+        anchor = lane_val(pd_e, npend - 1);
+        npend = 0;
+    };
     auto insert = [&](bool ins, uint32_t h, int32_t p) {   // distinct hashes among inserting lanes
         if (ins) {
             T16[h] = (uint16_t)(p & 0x7FFF);
@@ -1122,175 +1172,193 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T,
             atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
         }
     };
+    // 4 source bytes at x for the lanes that `need` them: from the window, else memory
+    auto seq_at = [&](int32_t x, bool need) -> uint32_t {
+        const int32_t ow = x - wb;
+        const bool inw = ow >= 0 && ow + 4 <= kWinBytes;
+        uint32_t v = 0;
+        if (need && inw) v = funnel(F.win[ow >> 2], F.win[(ow >> 2) + 1], (uint32_t)(ow & 3));
+        if (__ballot(need && !inw)) {   // (waited for here, not where the paths join: that wait would
+            if (need && !inw) v = ld_u32(j, x);   // also cover the previous batch's table stores)
+            wait_vmem();
+        }
+        settle32(v);
+        return v;
+    };
+    // window refill at base b: loads issued now (with a round trip's other loads), written after its wait
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+    auto refill_issue = [&](int32_t b) {
+        r0 = ld16(j, (int64_t)b + 16 * lane);
+        r1 = ld16(j, (int64_t)b + 1024 + 16 * lane);
+    };
+    auto refill_write = [&](int32_t b) {
+        settle32(r0.x); settle32(r0.y); settle32(r0.z); settle32(r0.w);
+        settle32(r1.x); settle32(r1.y); settle32(r1.z); settle32(r1.w);
+        *(uint4*)&F.win[4 * lane] = r0;
+        *(uint4*)&F.win[256 + 4 * lane] = r1;
+        wb = b;
+    };
     while (i < mflimit) {
         while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
         __builtin_amdgcn_s_setprio(3);
-        // ---- the batch: probes at i + kS, k < K, each assumed a hit of step S
-        int K = 1;
         if (c == 67 && S > 0) {
-            const int32_t lim = min(mflimit - 1, ((g + 1) << 15) - 1) - i;   // same epoch, before mflimit
-            K = 1 + lim / S;
-            if (K > kSpecK) K = kSpecK;
-        }
-        const bool act = lane < K;
-        const int32_t p = i + lane * S;
-        uint32_t seq = pf_seq;
-        {
-            const int32_t ow = p - wbase;
-            const bool inw = ow >= 0 && ow + 4 <= kSpecW;
-            const uint32_t ws = win_u32(wv, wl0, inw ? ow : 0);
-            if (inw) seq = ws;
-            if (__ballot(act && !inw && pf_pos != p)) {
-                if (act && !inw && pf_pos != p) seq = ld_u32(j, p);
+            // ================= hit batch: probes at i + kS, k < K, each assumed a hit of step S
+            int K;
+            {
+                const int32_t lim = min(mflimit - 1, ((g + 1) << 15) - 1) - i;   // same epoch, before mflimit
+                K = 1 + lim / S;
+                if (K > kSpecK) K = kSpecK;
             }
-        }
-        const uint32_t h = (seq * kP1) >> 18;
-        int32_t cand = -1;
-        bool dup = false;
-        for (int k = 0; k + 1 < K; ++k) {                       // an earlier probe of the batch with this hash
-            if (lane > k && lane_val(h, k) == h) {
-                cand = i + k * S;
-                dup = true;
+            const bool act = lane < K;
+            const int32_t p = i + lane * S;
+            const uint32_t seq = seq_at(p, act);
+            const uint32_t h = (seq * kP1) >> 18;
+            int32_t cand = -1;
+            bool dup = false;
+            // the latest earlier probe of the batch with this hash: row_shr:d (lanes 0..7 share row 0)
+#define LZ4MI_DUP(d)                                                   \
+            {                                                          \
+                const uint32_t hd = dpp<0x110 + d>(0xFFFFFFFFu, h);    \
+                if (!dup && lane >= d && hd == h) {                    \
+                    cand = p - d * S;                                  \
+                    dup = true;                                        \
+                }                                                      \
             }
-        }
-        const uint32_t litv = npend ? load_lit() : 0u;
-        CPROF(0);
-        CPROF_COUNT(8, 1);
-        uint32_t tlo = 0, tcd = 0;
-        if (act && !dup) {
-            tlo = T16[h];
-            tcd = gt_code_of(F, h);
-        }
-        if (npend) {                                            // off the chain, while the reads are in flight
-            __builtin_amdgcn_s_setprio(0);
-            emit_pending(litv);
-            __builtin_amdgcn_s_setprio(3);
-        }
-        // (the read's value is opaque until here: otherwise the compiler consumes it, and
-        // waits for it, right after the load, before the emission)
-        asm volatile("" : "+v"(tlo) :: "memory");
-        CPROF(1);
-        if (act && !dup) cand = gt16_decode(tlo, tcd, g);
-        if (cand >= 0 && (p - cand < 1 || p - cand > 65535)) cand = -1;
-        // ---- windows: lanes 8k .. 8k+7 hold 128 bytes at probe k and at its candidate
-        const int gk = lane >> 3, gt = lane & 7;
-        const int32_t gc = __shfl(cand, gk, kWave);
-        uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
-        if (gk < K) {
-            xa = ld16(j, (int64_t)i + gk * S + 16 * gt);
-            if (gc >= 0) xb = ld16(j, (int64_t)gc + 16 * gt);
-        }
-        {   // the next batch's probe bytes, assuming all K probes hit with step S
-            const int32_t q = i + (K + lane) * S;
-            pf_pos = (c == 67 && S > 0 && lane < kSpecK && q < mflimit) ? q : -1;
-            if (pf_pos >= 0) pf_seq = ld_u32(j, pf_pos);
-        }
-        CPROF(2);
-        wait_vmem();              // the windows and the prefetch (issued together): later uses never wait
-        settle32(pf_seq);
-        settle32(xa.x);
-        settle32(xa.y);
-        settle32(xa.z);
-        settle32(xa.w);
-        settle32(xb.x);
-        settle32(xb.y);
-        settle32(xb.z);
-        settle32(xb.w);
-        const uint32_t lm = (gk < K && gc >= 0) ? first_nz16(make_uint4(xa.x ^ xb.x, xa.y ^ xb.y, xa.z ^ xb.z, xa.w ^ xb.w))
-                                                : 0u;
-        const uint64_t mm = __ballot(lm < 16);
-        // lane k < K: bytes equal at probe k (m, 128 = the whole window)
-        const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
-        const int ft = gm ? __builtin_ctz(gm) : 0;
-        const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
-        const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
-        const bool hit = act && cand >= 0 && m >= 4;
-        const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;
-        const int32_t e = p + (m < matchlimit - p ? m : matchlimit - p);
-        const bool ok = hit && !lng && lane + 1 < K && e == p + S;
-        const int J = __builtin_ctzll(__ballot(act && !ok));   // the first probe that ends the batch
-        CPROF(3);
-        CPROF_COUNT(9, J);
-        // probes 0 .. J happened: each inserts its position (the last of equal hashes)
-        bool later = false;
-        for (int k = 1; k <= J; ++k)
-            if (k > lane && lane_val(h, k) == h) later = true;
-        insert(lane <= J && !later, h, p);
-        wbase = i + J * S;                                      // the miss chain reads its bytes from probe J's window
-        wl0 = 8 * J;
-        wv = xa;
-        const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
-        const bool hitJ = (__ballot(hit) >> J) & 1ull;
-        pd_p = p;
-        pd_c = cand;
-        pd_e = e;
-        CPROF(4);
-        if (hitJ) {
-            CPROF_COUNT(9, 1);
-            int32_t eJ = lane_val(e, J);
-            if ((__ballot(lng) >> J) & 1ull)
-                eJ = pJ + kSpecW + (int32_t)match_extent(j, lane, pJ + kSpecW, cJ + kSpecW, matchlimit - (pJ + kSpecW));
-            if (lane == J) pd_e = eJ;
-            npend = J + 1;
-            c = 67;                                             // (a single probe after a miss chain may hit)
-            CPROF(5);
-            S = eJ - pJ;
-            i = eJ;
+            LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7)
+#undef LZ4MI_DUP
+            static_assert(kSpecK == 8, "LZ4MI_DUP / LZ4MI_LATER cover distances 1..7");
+            const uint32_t litv = npend ? load_lit() : 0u;
+            CPROF(0);
+            CPROF_COUNT(8, 1);
+            uint32_t tlo = 0, tcd = 0;
+            if (act && !dup) {
+                tlo = T16[h];
+                tcd = gt_code_of(F, h);
+            }
+            if (npend) {                                        // off the chain, while the reads are in flight
+                __builtin_amdgcn_s_setprio(0);
+                emit_batch(litv);
+                __builtin_amdgcn_s_setprio(3);
+            }
+            // (the read's value is opaque until here: otherwise the compiler consumes it, and
+            // waits for it, right after the load, before the emission)
+            asm volatile("" : "+v"(tlo) :: "memory");
+            CPROF(1);
+            if (act && !dup) cand = gt16_decode(tlo, tcd, g);
+            if (cand >= 0 && (p - cand < 1 || p - cand > 65535)) cand = -1;
+            // ---- windows: lanes 8k .. 8k+7 hold 128 bytes at probe k and at its candidate
+            const int gk = lane >> 3, gt = lane & 7;
+            const int32_t gc = __shfl(cand, gk, kWave);
+            uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
+            if (gk < K) {
+                xa = ld16(j, (int64_t)i + gk * S + 16 * gt);
+                if (gc >= 0) xb = ld16(j, (int64_t)gc + 16 * gt);
+            }
+            const bool rf = (uint32_t)(i - wb) > 768u;          // the next batches' probes: window ahead
+            if (rf) refill_issue(i);
+            wait_vmem();
+            if (rf) refill_write(i);
+            CPROF(2);
+            const uint32_t lm = (gk < K && gc >= 0) ? first_nz16(make_uint4(xa.x ^ xb.x, xa.y ^ xb.y, xa.z ^ xb.z, xa.w ^ xb.w))
+                                                    : 0u;
+            const uint64_t mm = __ballot(lm < 16);
+            // lane k < K: bytes equal at probe k (m, 128 = the whole window)
+            const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
+            const int ft = gm ? __builtin_ctz(gm) : 0;
+            const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
+            const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
+            const bool hit = act && cand >= 0 && m >= 4;
+            const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;
+            const int32_t e = p + (m < matchlimit - p ? m : matchlimit - p);
+            const bool ok = hit && !lng && lane + 1 < K && e == p + S;
+            const int J = __builtin_ctzll(__ballot(act && !ok));   // the first probe that ends the batch
+            CPROF_COUNT(9, J);
+            // probes 0 .. J happened: each inserts its position (the last of equal hashes)
+            bool later = false;
+#define LZ4MI_LATER(d)                                                 \
+            {                                                          \
+                const uint32_t hd = dpp<0x100 + d>(0xFFFFFFFFu, h);    \
+                if (lane + d <= J && hd == h) later = true;            \
+            }
+            LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7)
+#undef LZ4MI_LATER
+            insert(lane <= J && !later, h, p);
+            const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
+            const bool hitJ = (__ballot(hit) >> J) & 1ull;
+            pd_p = p;
+            pd_c = cand;
+            pd_e = e;
+            CPROF(3);
+            if (hitJ) {
+                CPROF_COUNT(9, 1);
+                int32_t eJ = lane_val(e, J);
+                if ((__ballot(lng) >> J) & 1ull)
+                    eJ = pJ + kSpecW + (int32_t)match_extent(j, lane, pJ + kSpecW, cJ + kSpecW, matchlimit - (pJ + kSpecW));
+                if (lane == J) pd_e = eJ;
+                npend = J + 1;
+                S = eJ - pJ;
+                i = eJ;
+                CPROF(4);
+                continue;
+            }
+            // probe J missed (and inserted itself): the accepted hits go out, the miss chain
+            // goes on at the next position
+            npend = J;
+            if (npend) emit_pending(load_lit());
+            i = pJ + 1;                                         // (c = 67: step 1)
+            c = 68;
+            S = 0;
+            CPROF(4);
             continue;
         }
-        // ---- probe J missed (and inserted itself): the accepted hits go out, then the
-        // next probes of the miss chain as a batch
-        CPROF_COUNT(10, 1);
-        npend = J;
+        // ================= miss batch: the next 64 probes of the miss chain, starting at i
         if (npend) emit_pending(load_lit());
-        CPROF(6);
-        i = pJ + (int32_t)(c >> 6);
-        c += 1;
-        if (i >= mflimit) break;
-        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+        CPROF_COUNT(10, 1);
         const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
         const uint32_t step = (c + lane) >> 6;
         bool mact = pm_ < mflimit && (pm_ >> 15) == g;          // probes of the next epoch: the next batch
-        uint32_t mseq = 0;
-        {
-            const int32_t ow = pm_ - wbase;
-            const bool inw = ow >= 0 && ow + 4 <= kSpecW;
-            mseq = win_u32(wv, wl0, inw ? ow : 0);
-            if (__ballot(mact && !inw)) {
-                if (mact && !inw) mseq = ld_u32(j, pm_);
-            }
-        }
+        const uint32_t mseq = seq_at(pm_, mact);
         const uint32_t mh = (mseq * kP1) >> 18;
-        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
+        int nb = __popcll(__ballot(mact));
+        {   // cut the batch before the first lane whose hash repeats an earlier lane's: a lane-id
+            // map keyed by hash & 1023 flags the lanes that lost their slot; every true repeat
+            // group has such a lane, whose hash is then compared with all lanes' (exact)
             volatile uint8_t* vs = F.slot;
             if (mact) vs[mh & 1023] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
-            const bool mdup = mact && vs[mh & 1023] != (uint8_t)lane;
-            int nb = __popcll(__ballot(mact));
-            const uint64_t dm = __ballot(mdup);
-            if (dm) {
-                const int d = __builtin_ctzll(dm);
-                nb = d ? d : 1;
+            const bool lost = mact && vs[mh & 1023] != (uint8_t)lane;
+            for (uint64_t fm = __ballot(lost); fm; fm &= fm - 1) {
+                const uint32_t hf = lane_val(mh, __builtin_ctzll(fm));
+                const uint64_t same = __ballot(mact && mh == hf);
+                const uint64_t rest = same & (same - 1);       // all but the group's first lane
+                if (rest) {
+                    const int d = __builtin_ctzll(rest);
+                    if (d < nb) nb = d;
+                }
             }
             mact = mact && lane < nb;
         }
-        const int nb = __popcll(__ballot(mact));
+        CPROF(5);
         int32_t mc = -1;
         if (mact) {
             mc = gt16_decode(T16[mh], gt_code_of(F, mh), g);
             if (mc < 0 || pm_ - mc < 1 || pm_ - mc > 65535) mc = -1;
         }
         const uint32_t vw = mc >= 0 ? ld_u32(j, mc) : 0u;
+        const int32_t inext = lane_val(pm_ + (int32_t)step, nb - 1);   // where a batch without a hit goes on
+        const bool rf = (uint32_t)(i - wb) > 512u;              // the window for what follows either way
+        if (rf) refill_issue(i);
         const uint64_t hm = __ballot(mc >= 0 && vw == mseq);
+        if (rf) refill_write(i);
         const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
         insert(lane < nprobe, mh, pm_);                         // the probes that happen
+        CPROF(6);
         if (!hm) {
-            i = lane_val(pm_ + (int32_t)step, nb - 1);
+            i = inext;
             c += nb;
-            S = 0;
-            CPROF(7);
             continue;
         }
+        CPROF_COUNT(11, 1);
         const int mi = nprobe - 1;
         const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
         c = 67;
@@ -1310,12 +1378,12 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtShared& F, int32_t* T,
     if (npend) emit_pending(load_lit());
     o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
     return o.op;
 }
 
 __global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, int32_t* tables) {
-    __shared__ GtShared F;
+    __shared__ GtsShared F;
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
     CompJob j;
@@ -1511,7 +1579,7 @@ __device__ int64_t compress_block_chain(const CompJob& j, ChainShared& F, int la
     if (pv) emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
     o = emit_tail<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, &r);
     ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & kRingMask];
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
     CPROF(4);
 #if LZ4MI_CPROFILE
     if (lane == 0)

@@ -5,7 +5,7 @@ import argparse, ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "divortio-lz4_amd"))
 BLOCK = 4 << 20
-NAMES = ["seq+hash", "table issue+emit", "table wait", "windows", "validate", "insert", "miss emit", "miss chain"]
+NAMES = ["hit: seq+hash", "hit: table+emit", "hit: windows", "hit: validate+insert", "hit: end", "miss: seq+dedupe", "miss: table+verify", "miss: extend"]
 
 def main():
     ap = argparse.ArgumentParser()
@@ -39,10 +39,10 @@ def main():
             ms = e0.elapsed_time(e1)
             L.lz4mi_debug_cprof(buf)
             v = list(buf)
-            nb, hits, miss = v[8], v[9], v[10]
-            print(f"{gen} blocks={n} kernel_ms={ms:.1f} batches/block={nb / n:.0f} batch-hits/block={hits / n:.0f} "
-                  f"hits/batch={hits / max(1, nb):.2f} miss-chain entries/block={miss / n:.0f}")
-            print("   ns per batch:", {NAMES[i]: round(v[i] * 10 / max(1, nb), 1) for i in range(8)},
+            nb, hits, miss, mhit = v[8], v[9], v[10], v[11]
+            print(f"{gen} blocks={n} kernel_ms={ms:.1f} hit batches/block={nb / n:.0f} hits/hit batch={hits / max(1, nb):.2f} "
+                  f"miss batches/block={miss / n:.0f} (with a hit: {mhit / n:.0f})")
+            print("   us per block:", {NAMES[i]: round(v[i] / 100.0 / n, 1) for i in range(8)},
                   "wave ms:", round(sum(v[:8]) / 100.0 / n / 1000, 1), flush=True)
 
 if __name__ == "__main__":
