@@ -1075,6 +1075,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     int32_t i = 0, anchor = 0;
     uint32_t c = 67;
     int32_t S = 0;                       // step of the last hit (0: in a miss chain): the speculated probe distance
+    const int kmax = kSpecK;
     // accepted sequences not emitted yet (lanes 0 .. npend-1: probe, candidate, match end),
     // emitted while the next batch's table reads are in flight
     int npend = 0;
@@ -1207,7 +1208,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             {
                 const int32_t lim = min(mflimit - 1, ((g + 1) << 15) - 1) - i;   // same epoch, before mflimit
                 K = 1 + lim / S;
-                if (K > kSpecK) K = kSpecK;
+                if (K > kmax) K = kmax;
             }
             const bool act = lane < K;
             const int32_t p = i + lane * S;
@@ -1224,7 +1225,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
                     dup = true;                                        \
                 }                                                      \
             }
-            LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7)
+            if (K > 1) { LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7) }
 #undef LZ4MI_DUP
             static_assert(kSpecK == 8, "LZ4MI_DUP / LZ4MI_LATER cover distances 1..7");
             const uint32_t litv = npend ? load_lit() : 0u;
@@ -1280,7 +1281,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
                 const uint32_t hd = dpp<0x100 + d>(0xFFFFFFFFu, h);    \
                 if (lane + d <= J && hd == h) later = true;            \
             }
-            LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7)
+            if (J > 0) { LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7) }
 #undef LZ4MI_LATER
             insert(lane <= J && !later, h, p);
             const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
@@ -1588,6 +1589,258 @@ __device__ int64_t compress_block_chain(const CompJob& j, ChainShared& F, int la
     return o.op;
 }
 
+// The dependent-block chain with compress_block_gts's batching (round 3): hit batches of up to
+// kSpecK probes of one step, miss batches starting at the probe itself with the exact duplicate
+// cut, one ring write per batch of sequences. Everything it reads is in LDS: the table (int32,
+// the reference's values), the source ring (windows and probe bytes: aligned dword reads), the
+// output ring; one wave walks the frame, so a batch's cost is its instruction latency.
+__device__ __forceinline__ uint32_t ring_dw(uint32_t wi) { return ((const uint32_t*)g_ring)[wi]; }
+
+// 16 source bytes at p: from the ring while it holds them, else global memory.
+__device__ __forceinline__ uint4 rr16(const CompJob& j, const Ring& r, int64_t p) {
+    if (p >= r.lo && p + 16 <= r.hi) {
+        constexpr uint32_t W = kRingBytes / 4;
+        const uint32_t q = (uint32_t)(p % kRingBytes), w0 = q >> 2, sh = q & 3;
+        uint32_t d[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t x = w0 + k;
+            d[k] = ring_dw(x >= W ? x - W : x);
+        }
+        return make_uint4(funnel(d[0], d[1], sh), funnel(d[1], d[2], sh), funnel(d[2], d[3], sh), funnel(d[3], d[4], sh));
+    }
+    return ld16(j, p);
+}
+__device__ __forceinline__ uint32_t rr32(const CompJob& j, const Ring& r, int64_t p) {
+    if (p >= r.lo && p + 4 <= r.hi) {
+        constexpr uint32_t W = kRingBytes / 4;
+        const uint32_t q = (uint32_t)(p % kRingBytes), w0 = q >> 2;
+        const uint32_t w1 = w0 + 1 >= W ? 0u : w0 + 1;
+        return funnel(ring_dw(w0), ring_dw(w1), q & 3);
+    }
+    return ld_u32(j, p);
+}
+
+// match_extent with its first 256 bytes read from the ring (one step of 4 bytes per lane).
+__device__ int64_t match_extent_ring(const CompJob& j, const Ring& r, int lane, int64_t a, int64_t b, int64_t lim) {
+    const uint32_t x = rr32(j, r, a + 4 * lane) ^ rr32(j, r, b + 4 * lane);
+    const uint64_t m = __ballot(x != 0);
+    if (m) {
+        const int fl = __builtin_ctzll(m);
+        const int64_t f = 4 * fl + (__builtin_ctz(lane_val(x, fl)) >> 3);
+        return f < lim ? f : lim;
+    }
+    if (lim <= 4 * kWave) return lim;
+    return 4 * kWave + match_extent(j, lane, a + 4 * kWave, b + 4 * kWave, lim - 4 * kWave);
+}
+
+__device__ int64_t compress_block_chain2(const CompJob& j, ChainShared& F, int lane, Ring& r) {
+    int32_t* T = g_ctab;
+    const int32_t start = j.start, end = j.start + j.len;
+    const int32_t mflimit = end - 12, matchlimit = end - 5;
+    FastOut o{j.dst, 0, 0};
+    int32_t i = start, anchor = start;
+    uint32_t c = 67;
+    int32_t S = 0;
+    const int kmax = kSpecK;
+    int npend = 0;
+    int32_t pd_p = 0, pd_c = 0, pd_e = 0;
+    auto emit_pending = [&](uint32_t litv) {
+        for (int k = 0; k < npend; ++k) {
+            const int32_t pm = lane_val(pd_p, k), cm = lane_val(pd_c, k), e = lane_val(pd_e, k);
+            emit_seq<ChainShared, SrcR>(F, o, j, lane, anchor, pm, (uint32_t)(pm - cm), e - pm - 4, &r, true, litv);
+            anchor = e;
+        }
+        npend = 0;
+    };
+    auto load_lit = [&]() -> uint32_t {
+        const int32_t lit0 = lane_val(pd_p, 0) - anchor;
+        const bool ld = lit0 > 0 && lit0 < 15 && lane >= 1 && lane <= lit0;
+        return ld ? SrcR::byte(j, &r, anchor + lane - 1) : 0u;
+    };
+    auto emit_batch = [&](uint32_t litv) {   // as compress_block_gts's
+        const int32_t lit0 = lane_val(pd_p, 0) - anchor;
+        const int32_t mcode = pd_e - pd_p - 4;
+        const bool mine = lane < npend;
+        if (lit0 >= 15 || __ballot(mine && mcode >= 15 + 255)) {
+            emit_pending(litv);
+            return;
+        }
+        const int32_t lit = lane == 0 ? lit0 : 0;
+        const uint32_t size = mine ? 3u + (uint32_t)lit + (mcode >= 15 ? 1u : 0u) : 0u;
+        uint32_t incl = size;
+        incl += dpp<kRowShr1>(0u, incl);
+        incl += dpp<kRowShr2>(0u, incl);
+        incl += dpp<kRowShr4>(0u, incl);
+        const uint32_t st = incl - size;
+        const int32_t total = (int32_t)lane_val(incl, npend - 1);
+        const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
+        const uint32_t off = (uint32_t)(pd_p - pd_c);
+        ring_reserve(F, o, lane, total);
+        int32_t rr = lane, cl = 0;
+        uint32_t ct = 0, co = 0, cm = 0;
+        for (int k = 0; k < npend; ++k) {
+            const int32_t sk = (int32_t)lane_val(st, k);
+            if (lane >= sk) {
+                rr = lane - sk;
+                cl = k == 0 ? lit0 : 0;
+                ct = lane_val(tok, k);
+                co = lane_val(off, k);
+                cm = (uint32_t)lane_val(mcode, k);
+            }
+        }
+        if (lane < total) {
+            uint32_t v;
+            if (rr == 0) v = ct;
+            else if (rr <= cl) v = litv;
+            else if (rr == cl + 1) v = co & 255;
+            else if (rr == cl + 2) v = (co >> 8) & 255;
+            else v = cm - 15;
+            F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
+        }
+        o.op += total;
+        anchor = lane_val(pd_e, npend - 1);
+        npend = 0;
+    };
+    while (i < mflimit) {
+        if (r.hi - i < kRingAhead) ring_advance(j, r, lane, i);
+        if (c == 67 && S > 0) {
+            // ================= hit batch
+            int K = __popcll(__ballot(lane < kmax && lane * S <= mflimit - 1 - i));
+            const bool act = lane < K;
+            const int32_t p = i + lane * S;
+            const uint32_t seq = act ? rr32(j, r, p) : 0u;
+            const uint32_t h = (seq * kP1) >> 18;
+            int32_t cand = -1;
+            bool dup = false;
+#define LZ4MI_DUP(d)                                                   \
+            {                                                          \
+                const uint32_t hd = dpp<0x110 + d>(0xFFFFFFFFu, h);    \
+                if (!dup && lane >= d && hd == h) {                    \
+                    cand = p - d * S;                                  \
+                    dup = true;                                        \
+                }                                                      \
+            }
+            if (K > 1) { LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7) }
+#undef LZ4MI_DUP
+            if (act && !dup) {
+                const int32_t old = T[h];
+                cand = old - 1;
+                if (old <= 0) cand = -1;
+            }
+            if (cand >= 0 && (cand == p || (uint32_t)(p - cand) > 65535u)) cand = -1;
+            if (npend) emit_batch(load_lit());
+            const int gk = lane >> 3, gt = lane & 7;
+            const int32_t gc = __shfl(cand, gk, kWave);
+            uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
+            if (gk < K) {
+                xa = rr16(j, r, (int64_t)i + gk * S + 16 * gt);
+                if (gc >= 0) xb = rr16(j, r, (int64_t)gc + 16 * gt);
+            }
+            const uint32_t lm = (gk < K && gc >= 0) ? first_nz16(make_uint4(xa.x ^ xb.x, xa.y ^ xb.y, xa.z ^ xb.z, xa.w ^ xb.w))
+                                                    : 0u;
+            const uint64_t mm = __ballot(lm < 16);
+            const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
+            const int ft = gm ? __builtin_ctz(gm) : 0;
+            const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
+            const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
+            const bool hit = act && cand >= 0 && m >= 4;
+            const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;
+            const int32_t e = p + (m < matchlimit - p ? m : matchlimit - p);
+            const bool ok = hit && !lng && lane + 1 < K && e == p + S;
+            const int J = __builtin_ctzll(__ballot(act && !ok));
+            bool later = false;
+#define LZ4MI_LATER(d)                                                 \
+            {                                                          \
+                const uint32_t hd = dpp<0x100 + d>(0xFFFFFFFFu, h);    \
+                if (lane + d <= J && hd == h) later = true;            \
+            }
+            if (J > 0) { LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7) }
+#undef LZ4MI_LATER
+            __builtin_amdgcn_wave_barrier();
+            if (lane <= J && !later) T[h] = p + 1;
+            __builtin_amdgcn_wave_barrier();
+            const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
+            const bool hitJ = (__ballot(hit) >> J) & 1ull;
+            pd_p = p;
+            pd_c = cand;
+            pd_e = e;
+            if (hitJ) {
+                int32_t eJ = lane_val(e, J);
+                if ((__ballot(lng) >> J) & 1ull)
+                    eJ = pJ + kSpecW + (int32_t)match_extent_ring(j, r, lane, pJ + kSpecW, cJ + kSpecW, matchlimit - (pJ + kSpecW));
+                if (lane == J) pd_e = eJ;
+                npend = J + 1;
+                S = eJ - pJ;
+                i = eJ;
+                continue;
+            }
+            npend = J;
+            if (npend) emit_batch(load_lit());
+            i = pJ + 1;
+            c = 68;
+            S = 0;
+            continue;
+        }
+        // ================= miss batch
+        if (npend) emit_batch(load_lit());
+        const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const uint32_t step = (c + lane) >> 6;
+        bool mact = pm_ < mflimit;
+        const uint32_t mseq = mact ? SrcR::u32(j, &r, pm_) : 0u;
+        const uint32_t mh = (mseq * kP1) >> 18;
+        int nb = __popcll(__ballot(mact));
+        {
+            volatile uint8_t* vs = F.slot;
+            if (mact) vs[mh & 1023] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool lost = mact && vs[mh & 1023] != (uint8_t)lane;
+            for (uint64_t fm = __ballot(lost); fm; fm &= fm - 1) {
+                const uint32_t hf = lane_val(mh, __builtin_ctzll(fm));
+                const uint64_t same = __ballot(mact && mh == hf);
+                const uint64_t rest = same & (same - 1);
+                if (rest) {
+                    const int d = __builtin_ctzll(rest);
+                    if (d < nb) nb = d;
+                }
+            }
+            mact = mact && lane < nb;
+        }
+        int32_t mc = -1;
+        if (mact) {
+            const int32_t ov = T[mh];
+            mc = ov - 1;
+            if (ov <= 0 || mc == pm_ || (uint32_t)(pm_ - mc) > 65535u) mc = -1;
+        }
+        const uint32_t vw = mc >= 0 ? SrcR::u32(j, &r, mc) : 0u;
+        const uint64_t hm = __ballot(mc >= 0 && vw == mseq);
+        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nprobe) T[mh] = pm_ + 1;
+        __builtin_amdgcn_wave_barrier();
+        if (!hm) {
+            i = lane_val(pm_ + (int32_t)step, nb - 1);
+            c += nb;
+            continue;
+        }
+        const int mi = nprobe - 1;
+        const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
+        c = 67;
+        const int32_t e1 = pm + 4 + (int32_t)match_extent_ring(j, r, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
+        pd_p = pm;
+        pd_c = cm;
+        pd_e = e1;
+        npend = 1;
+        S = e1 - pm;
+        i = e1;
+    }
+    if (npend) emit_batch(load_lit());
+    o = emit_tail<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, &r);
+    ring_flush(F, o, lane);
+    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
+    return o.op;
+}
+
 struct ChainArgs {
     const uint8_t* src;
     uint64_t src_total;
@@ -1597,6 +1850,7 @@ struct ChainArgs {
     const uint64_t* out_off;
     uint32_t* comp_len;
     uint32_t nblocks;
+    int v1;               // 1: the one-sequence-per-step chain (A/B)
 };
 
 __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
@@ -1613,7 +1867,7 @@ __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
         const int32_t n = (int32_t)(rest < a.bsize ? rest : a.bsize);
         CompJob j{a.src, a.src_total, (int32_t)s0, n, a.out + a.out_off[b],
                   (uint64_t)n + (uint64_t)n / 255u + 16u, 0, nullptr};
-        const int64_t w = compress_block_chain(j, F, lane, r);
+        const int64_t w = a.v1 ? compress_block_chain(j, F, lane, r) : compress_block_chain2(j, F, lane, r);
         if (lane == 0) a.comp_len[b] = (uint32_t)w;
     }
     __syncthreads();
@@ -1668,7 +1922,9 @@ extern "C" hipError_t lz4mi_launch_compress_chain(const uint8_t* src, uint64_t s
                                                   int32_t bsize, int32_t* table, uint8_t* out, const uint64_t* out_off,
                                                   uint32_t* comp_len, uint32_t nblocks, hipStream_t stream) {
     if (nblocks == 0) return hipSuccess;
-    lz4mi::ChainArgs a{src, src_total, start, len, bsize, table, out, out_off, comp_len, nblocks};
+    const char* v = getenv("LZ4MI_CHAIN");   // LZ4MI_CHAIN=v1: the one-sequence-per-step chain (A/B)
+    lz4mi::ChainArgs a{src, src_total, start, len, bsize, table, out, out_off, comp_len, nblocks,
+                       (v && v[0] == 'v' && v[1] == '1') ? 1 : 0};
     hipLaunchKernelGGL(lz4mi::lz4mi_compress_chain_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
