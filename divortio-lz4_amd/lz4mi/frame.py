@@ -152,6 +152,42 @@ def _shm_dir():
     return "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
 
 
+def _shm_free():
+    try:
+        st = os.statvfs(_shm_dir())
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return 0
+
+
+def _sent_checksum(shard, sizes, dist, group, world, rank, root, seed):
+    """staged_checksum's route when the shared memory filesystem cannot hold the shards:
+    every other rank sends its shard to root in _STAGE_PIECE pieces over the group (device
+    tensors over RCCL with the nccl backend), root hashes them in rank order as they come."""
+    import torch
+    g = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    if rank != root:
+        n = shard.numel()
+        for p in range(0, n, _STAGE_PIECE):
+            dist.send(shard[p:p + _STAGE_PIECE].contiguous(), dst=g(root), group=group)
+        return None
+    w = _ChecksumWorker(seed)
+    for r in range(world):
+        if r == root:
+            for a in _host_pieces(shard):
+                w.feed(a)
+            continue
+        if not sizes[r]:
+            continue
+        buf = torch.empty(min(_STAGE_PIECE, sizes[r]), dtype=torch.uint8, device=shard.device)
+        for p in range(0, sizes[r], _STAGE_PIECE):
+            m = min(_STAGE_PIECE, sizes[r] - p)
+            dist.recv(buf[:m], src=g(r), group=group)
+            for a in _host_pieces(buf[:m]):
+                w.feed(a.copy())     # the pinned piece is reused by the next recv
+    return w.digest()
+
+
 def _host_pieces(t, piece=_STAGE_PIECE, nbuf=4):
     """Numpy views of consecutive pieces of a 1-D uint8 tensor. A device tensor goes through
     `nbuf` rotating pinned buffers (full-rate device-to-host copies); a piece's buffer is
@@ -192,6 +228,14 @@ def staged_checksum(shard, group=None, root=0, seed=0):
     all_n = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(all_n, t, group=group)
     sizes = [int(x.item()) for x in all_n]
+    # every rank must agree on the staging route before anyone writes: the segments of all
+    # non-root ranks must fit the shared memory filesystem (a memmap write past a full tmpfs
+    # is a SIGBUS, not an exception), else the shards go to root piece by piece over the group
+    need = sum(sizes[r] for r in range(world) if r != root)
+    ok = torch.tensor([1 if _shm_free() >= need + (1 << 30) else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if not int(ok.item()):
+        return _sent_checksum(shard, sizes, dist, group, world, rank, root, seed)
     _stage_calls[0] += 1
     tag = torch.tensor([os.getpid(), _stage_calls[0]], dtype=torch.int64, device=dev)
     dist.broadcast(tag, src=dist.get_global_rank(group, root) if group is not None else root, group=group)

@@ -158,6 +158,14 @@ def _frame_worker(rank, world, port, q):
             # the host-staged content checksum alone == the oracle's XXH32 of the whole input
             d = F.staged_checksum(mine)
             ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
+            # the same when the shared memory filesystem is too small: shards sent to the root
+            real_free = F._shm_free
+            F._shm_free = lambda: 0
+            try:
+                d = F.staged_checksum(mine)
+            finally:
+                F._shm_free = real_free
+            ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
             res.append((ok, ok_back))
         q.put((rank, res))
         dist.barrier()

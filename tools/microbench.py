@@ -108,6 +108,7 @@ def main():
         st = torch.zeros(n, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
         cbytes = int(clen.sum())
+        ref = (comp.clone(), clen.clone()) if args.what != "decompress" else None
         for name, L in libs:
             def run():
                 if args.what == "decompress":
@@ -132,6 +133,9 @@ def main():
             ok = True
             if args.what == "decompress":
                 ok = bool(torch.equal(dec, raw)) and bool((st == 0).all())
+            else:   # byte-identical to the first build's output (the bytes past each block's
+                #     length are the same leftovers in both buffers)
+                ok = bool(torch.equal(clen, ref[1])) and bool(torch.equal(comp, ref[0]))
             t = sorted(times)[len(times) // 2]
             res[f"{gen}/{name}"] = {"ms": round(t * 1e3, 3), "GBps": round(n * BLOCK / t / 1e9, 1),
                                     "hbm_frac": round((n * BLOCK + cbytes) / t / 8e12, 4), "ok": ok,

@@ -6,7 +6,7 @@
 set -o pipefail
 OUT=$1; GEN=${2:-tiles216}; WHAT=${3:-decompress}
 KERNEL=lz4mi_decompress_kernel
-[ "$WHAT" = compress ] && KERNEL=lz4mi_compress_gt_kernel
+[ "$WHAT" = compress ] && KERNEL=lz4mi_compress_gts_kernel
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
 for pmc in FETCH_SIZE WRITE_SIZE; do
