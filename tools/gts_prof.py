@@ -3,6 +3,7 @@
 Build: FILE=lz4mi_compress.hip tools/build_variant.sh cprof 's/^#define LZ4MI_CPROFILE 0 /#define LZ4MI_CPROFILE 1 /'"""
 import argparse, ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "divortio-lz4_amd"))
 BLOCK = 4 << 20
 NAMES = ["hit: seq+hash", "hit: table+emit", "hit: windows", "hit: validate+insert", "hit: end", "miss: seq+dedupe", "miss: table+verify", "miss: extend"]
@@ -22,9 +23,9 @@ def main():
     s = torch.cuda.Stream(); torch.cuda.set_stream(s); sp = s.cuda_stream
     buf = (ctypes.c_ulonglong * 16)()
     for gen in a.gens.split(","):
+        from microbench import make_raw
         for n in map(int, a.blocks.split(",")):
-            raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-            lz4mi.generate_blocks_dev(raw.data_ptr(), gen, 1, BLOCK, n, sp)
+            raw = make_raw(torch, lz4mi, gen, n, sp)   # device generators, or host-made (text, copy, ...)
             slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
             comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
             roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
