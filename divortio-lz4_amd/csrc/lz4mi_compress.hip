@@ -429,17 +429,10 @@ __global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
 // are copied global -> global directly. No vector-memory store precedes the
 // next probe's loads except at ring flushes.
 constexpr int kCodeWords = 16384 / 16;
-constexpr int kRing = 4096;
-constexpr int kRingMask = kRing - 1;
 #define RING_SZ(F) ((int64_t)sizeof((F).ring))   // the output ring's size in the caller's shared struct
 #define RING_MASK(F) (RING_SZ(F) - 1)
 constexpr int32_t kDirectLit = 2048;   // longer literal runs bypass the ring
 
-struct FastShared {
-    uint16_t lo[16384];
-    uint32_t code[kCodeWords];
-    uint8_t ring[kRing];
-};
 
 struct FastOut {
     uint8_t* dst;
@@ -542,20 +535,7 @@ __device__ void fast_literals(SH& F, FastOut& o, const CompJob& j, int lane, int
     if (lit) ring_copy<SH, SRC>(F, o, j, lane, anchor, lit, rg);
 }
 
-__device__ __forceinline__ uint32_t code_of(const FastShared& F, uint32_t h) {
-    return (F.code[h >> 4] >> ((h & 15) * 2)) & 3u;
-}
 
-// entering epoch g: fields with code g mod 4 (stale, 4 epochs old) -> code (g+1) mod 4
-__device__ void scrub_epoch(FastShared& F, int lane, int32_t g) {
-    const uint32_t X = (uint32_t)(g & 3) * 0x55555555u, Y = (uint32_t)((g + 1) & 3) * 0x55555555u;
-    for (int w = lane; w < kCodeWords; w += kWave) {
-        const uint32_t v = F.code[w], x = v ^ X;
-        const uint32_t eq = ~(x | (x >> 1)) & 0x55555555u;
-        const uint32_t fm = eq | (eq << 1);
-        F.code[w] = (v & ~fm) | (Y & fm);
-    }
-}
 
 // Sum over u < x of floor(u / 64): the miss-chain distance covered by the skip
 // steps (c + t) >> 6 is skip_sum(c + k) - skip_sum(c).
@@ -615,192 +595,13 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
     o = emit_general<SH, SRC>(F, o, j, lane, anchor, pm, off, mcode, rg);
 }
 
-__device__ int64_t compress_block_fast(const CompJob& j, FastShared& F, int lane) {
-    const int32_t n = j.len;
-    const int32_t mflimit = n - 12, matchlimit = n - 5;
-    FastOut o{j.dst, 0, 0};
-    int32_t i = 0, anchor = 0;
-    uint32_t c = 67;
-    int32_t g = 0;
-    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
-    uint32_t wl = 0;
-    // the previous match, emitted while the next probe's loads are in flight
-    bool pv = false;
-    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
-    uint32_t p_off = 0;
-    for (int k = lane; k < 16384; k += kWave) F.lo[k] = 0;
-    for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
-    __syncthreads();
-#if LZ4MI_CPROFILE
-    uint64_t cprof[10] = {0};
-    uint64_t cprof_t = wall_clock64();
-#endif
-    while (i < mflimit) {
-        CPROF(6);
-        CPROF_COUNT(8, 1);
-        while ((i >> 15) > g) scrub_epoch(F, lane, ++g);
-        // this batch's probe positions, assuming every probe misses
-        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
-        const uint32_t step = (c + lane) >> 6;
-        bool act = p < mflimit && (p >> 15) == g;
-        uint32_t seq = 0;
-        {   // from the window when it holds [p, p+4), else from memory
-            const int32_t off = p - wb;
-            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
-            const int wi = inw ? (off >> 2) : 0;
-            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
-            seq = funnel(w0, w1, (uint32_t)(off & 3));
-            if (__ballot(act && !inw)) {
-                if (act && !inw) seq = ld_u32(j, p);
-            }
-        }
-        const uint32_t h = (seq * kP1) >> 18;
-        uint32_t lo = 0, cd = 0;
-        if (act) { lo = F.lo[h]; cd = code_of(F, h); }
-        CPROF(0);
-        int nb = __popcll(__ballot(act));                     // active lanes are a prefix
-        int32_t cand = -1;
-        if (act && cd != (uint32_t)((g + 1) & 3)) {
-            const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
-            cand = (ge << 15) | (int32_t)(lo & 0x7FFFu);
-            if (ge < 0 || p - cand < 1 || p - cand > 65535) cand = -1;
-        }
-        CPROF(1);
-        // verification loads, and (speculating that the first probe hits) the
-        // 256-byte extension windows of lane 0's candidate, in one round trip
-        const int32_t c0 = lane_val(cand, 0);
-        const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
-        uint32_t aw = 0, bw = 0;
-        if (c0 >= 0) {
-            aw = ld_u32(j, (int64_t)i + 4 + 4 * lane);
-            bw = ld_u32(j, (int64_t)c0 + 4 + 4 * lane);
-        }
-        if (pv) {                                             // overlaps the loads above
-            emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-            pv = false;
-        }
-        uint64_t hm = __ballot(cand >= 0 && vw == seq);
-        CPROF(2);
-        if (!(hm & 1ull) && nb > 1) {
-            // the first probe missed: a later lane's table read is only right if no
-            // earlier lane of the batch shares its hash (that probe would insert
-            // first). Write lane ids, read back: where ids collide, cut the batch
-            // before the first colliding lane. (volatile: the read-back must see
-            // other lanes' writes, not this lane's own value forwarded)
-            volatile uint16_t* vlo = F.lo;
-            if (act) vlo[h] = (uint16_t)lane;
-            __builtin_amdgcn_wave_barrier();
-            const bool dup = act && vlo[h] != (uint16_t)lane;
-            __builtin_amdgcn_wave_barrier();
-            if (act) vlo[h] = (uint16_t)lo;
-            const uint64_t dm = __ballot(dup);
-            if (dm) {
-                const int d = __builtin_ctzll(dm);
-                nb = d ? d : 1;
-                hm &= (nb >= 64) ? ~0ull : ((1ull << nb) - 1);
-            }
-        }
-        CPROF(3);
-        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
-        if (lane < nprobe) {                                  // the probes that happen insert their position
-            F.lo[h] = (uint16_t)(p & 0xFFFF);
-            const uint32_t sh = (h & 15) * 2;
-            atomicAnd(&F.code[h >> 4], ~(3u << sh));
-            atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
-        }
-        if (!hm) {
-            i = lane_val(p + (int32_t)step, nb - 1);
-            c += nb;
-            continue;
-        }
-        CPROF(4);
-        CPROF_COUNT(9, 1);
-        const int m = nprobe - 1;
-        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
-        c = 67;
-        const int32_t lim = matchlimit - (pm + 4);
-        int32_t f;
-        if (m == 0) {                     // extension from the speculative windows
-            const uint32_t x = aw ^ bw;
-            const uint64_t xm = __ballot(x != 0);
-            if (xm) {
-                const int fl = __builtin_ctzll(xm);
-                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
-            } else {
-                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, pm + 4 + 4 * kWave,
-                                                                        cm + 4 + 4 * kWave, lim - 4 * kWave)
-                                    : lim;
-            }
-            if (f > lim) f = lim;
-            wb = pm + 4;                  // the next probes' bytes come from this window
-            wl = aw;
-        } else {
-            f = (int32_t)match_extent(j, lane, pm + 4, cm + 4, lim);
-        }
-        const int32_t e = pm + 4 + f;
-        CPROF(5);
-        pv = true;
-        p_anchor = anchor;
-        p_pm = pm;
-        p_off = (uint32_t)(pm - cm);
-        p_mcode = e - pm - 4;
-        i = e;
-        anchor = e;
-    }
-    if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-    CPROF(6);
-#if LZ4MI_CPROFILE
-    if (lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
-#endif
-    o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
-    ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
-    return o.op;
-}
-
-__global__ __launch_bounds__(64) void lz4mi_compress_fast_kernel(CompArgs a) {
-    __shared__ FastShared F;
-    const uint32_t b = blockIdx.x;
-    if (b >= a.nblocks) return;
-    CompJob j;
-    j.src = a.in + a.in_off[b];
-    j.src_total = a.in_len[b];
-    j.start = 0;
-    j.len = (int32_t)a.in_len[b];
-    j.dst = a.out + a.out_off[b];
-    j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
-    j.dst_pos = 0;
-    j.table = nullptr;
-    const int64_t r = compress_block_fast(j, F, threadIdx.x);
-    if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
-}
 
 // ---------------------------------------------------------------------------
-// Batch encoder with the hash tables in global memory: one Int32Array(16384)
-// per block (values = position + 1, as the reference's), so LDS only holds the
-// output ring and 16 blocks run per CU instead of 4. A probe at the chain's
-// head reads and replaces its table slot (the reference's insert-before-verify);
-// after a miss the following probes go as a 64-wide batch like
-// compress_block_fast's (the probes that happen store their positions, and the
-// stores complete before the next table access). Table reads are plain loads:
-// the CU's L1 sees the wave's own completed stores (nontemporal loads and an
-// atomic exchange at the head, used until round 2, cost 7 %: 208.8 vs 194.5 ms).
-#ifndef LZ4MI_GT16
-#define LZ4MI_GT16 1   // 1: the batch encoder's tables as 15-bit positions in global + 2-bit epoch codes in LDS
-#endif
-
-struct GtShared {
-    uint8_t ring[kRing];
-    uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
-#if LZ4MI_GT16
-    uint32_t code[kCodeWords];   // 2-bit epoch code per table entry (as FastShared's)
-#endif
-};
-
-#if LZ4MI_GT16
-// A 15-bit table entry + its epoch code -> the position it stands for (-1: empty/stale),
-// exactly as compress_block_fast decodes its LDS table.
+// Batch encoder tables: one per block in global scratch, each entry the probed
+// position's low 15 bits (32 KiB per block) plus a 2-bit code of its 32 KiB epoch in
+// LDS (4 KiB per block). Epochs g-2..g decode uniquely; entering epoch g relabels the
+// codes 4 epochs old as stale. A 15-bit entry + its code -> the position it stands
+// for (-1: empty/stale).
 __device__ __forceinline__ int32_t gt16_decode(uint32_t lo, uint32_t cd, int32_t g) {
     if (cd == (uint32_t)((g + 1) & 3)) return -1;
     const int32_t ge = g - (int32_t)((g - (int32_t)cd) & 3);
@@ -820,206 +621,13 @@ __device__ void gt_scrub_epoch(SH& F, int lane, int32_t g) {
         F.code[w] = (v & ~fm) | (Y & fm);
     }
 }
-#endif
 
-__device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, int lane) {
-    const int32_t n = j.len;
-    const int32_t mflimit = n - 12, matchlimit = n - 5;
-    FastOut o{j.dst, 0, 0};
-    int32_t i = 0, anchor = 0;
-    uint32_t c = 67;
-    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
-    uint32_t wl = 0;
-    bool pv = false;             // the previous match, emitted while the next probe's loads are in flight
-    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
-    uint32_t p_off = 0;
-#if LZ4MI_GT16
-    uint16_t* T16 = (uint16_t*)T;   // 32 KiB of the block's 64 KiB slot
-    int32_t g = 0;                  // epoch of the parse position (32 KiB each)
-    for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
-    for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
-#else
-    for (int k = lane; k < 16384 / 4; k += kWave) ((uint4*)T)[k] = make_uint4(0, 0, 0, 0);
-#endif
-    wait_vmem();                 // the table is zero before the first exchange
-    while (i < mflimit) {
-#if LZ4MI_GT16
-        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
-#endif
-        // ---- the probe at i: one exchange, then verification + speculative extension windows
-        // high wave priority on the chain (probe, hit test, extension); the previous
-        // sequence's emission below, off the chain, runs at low priority while its loads
-        // are in flight: tiles216 -2.1 % (A/B in one process, profiles/r02j/compress_prio_ab.json)
-        __builtin_amdgcn_s_setprio(3);
-        const int32_t off0 = i - wb;
-        uint32_t seq0;
-        if (off0 >= 0 && off0 + 4 <= 4 * kWave) {
-            const int wi = off0 >> 2;
-            seq0 = funnel(__builtin_amdgcn_readlane(wl, wi), __builtin_amdgcn_readlane(wl, wi < kWave - 1 ? wi + 1 : wi),
-                          (uint32_t)(off0 & 3));
-        } else {
-            seq0 = uniform(ld_u32(j, i));
-        }
-        const uint32_t h0 = (seq0 * kP1) >> 18;
-#if LZ4MI_GT16
-        int32_t cand0 = -1;
-        if (lane == 0) {   // read and replace: 15-bit position in global, epoch code in LDS
-            cand0 = gt16_decode(T16[h0], gt_code_of(F, h0), g);
-            T16[h0] = (uint16_t)(i & 0x7FFF);
-            const uint32_t sh = (h0 & 15) * 2;
-            F.code[h0 >> 4] = (F.code[h0 >> 4] & ~(3u << sh)) | ((uint32_t)(g & 3) << sh);
-        }
-        cand0 = (int32_t)uniform((uint32_t)cand0);
-        if (cand0 < 0 || i - cand0 < 1 || i - cand0 > 65535) cand0 = -1;
-#else
-        int32_t old = 0;
-        if (lane == 0) {   // read and replace (one wave owns the table: no atomic needed)
-            old = T[h0];
-            T[h0] = i + 1;
-        }
-        old = (int32_t)uniform((uint32_t)old);
-        int32_t cand0 = old - 1;
-        if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
-#endif
-        uint32_t aw = 0, bw = 0;
-        bool hit0 = false;
-        if (cand0 >= 0) {
-            const uint32_t vw = ld_u32(j, cand0);
-            aw = ld_u32(j, (int64_t)i + 4 + 4 * lane);
-            bw = ld_u32(j, (int64_t)cand0 + 4 + 4 * lane);
-            if (pv) {
-                __builtin_amdgcn_s_setprio(0);
-                emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-                __builtin_amdgcn_s_setprio(3);
-                pv = false;
-            }
-            hit0 = uniform(vw) == seq0;
-        }
-        if (hit0) {
-            c = 67;
-            const int32_t lim = matchlimit - (i + 4);
-            const uint32_t x = aw ^ bw;
-            const uint64_t xm = __ballot(x != 0);
-            int32_t f;
-            if (xm) {
-                const int fl = __builtin_ctzll(xm);
-                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
-            } else {
-                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, i + 4 + 4 * kWave,
-                                                                        cand0 + 4 + 4 * kWave, lim - 4 * kWave)
-                                    : lim;
-            }
-            if (f > lim) f = lim;
-            wb = i + 4;
-            wl = aw;
-            const int32_t e = i + 4 + f;
-            pv = true;
-            p_anchor = anchor;
-            p_pm = i;
-            p_off = (uint32_t)(i - cand0);
-            p_mcode = e - i - 4;
-            i = e;
-            anchor = e;
-            continue;
-        }
-        if (pv) {
-            emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-            pv = false;
-        }
-        // ---- the probe at i missed (and inserted itself): the next probes of the miss chain as a batch
-        i += (int32_t)(c >> 6);
-        c += 1;
-        if (i >= mflimit) break;
-        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
-        const uint32_t step = (c + lane) >> 6;
-#if LZ4MI_GT16
-        while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
-        bool act = p < mflimit && (p >> 15) == g;   // probes of the next epoch: the next batch
-#else
-        bool act = p < mflimit;
-#endif
-        uint32_t seq = 0;
-        {
-            const int32_t off = p - wb;
-            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
-            const int wi = inw ? (off >> 2) : 0;
-            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
-            seq = funnel(w0, w1, (uint32_t)(off & 3));
-            if (__ballot(act && !inw)) {
-                if (act && !inw) seq = ld_u32(j, p);
-            }
-        }
-        const uint32_t h = (seq * kP1) >> 18;
-        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
-            volatile uint8_t* vs = F.slot;
-            if (act) vs[h & 1023] = (uint8_t)lane;
-            __builtin_amdgcn_wave_barrier();
-            const bool dup = act && vs[h & 1023] != (uint8_t)lane;
-            int nb = __popcll(__ballot(act));
-            const uint64_t dm = __ballot(dup);
-            if (dm) {
-                const int d = __builtin_ctzll(dm);
-                nb = d ? d : 1;
-            }
-            act = act && lane < nb;
-        }
-        const int nb = __popcll(__ballot(act));
-        int32_t cand = -1;
-#if LZ4MI_GT16
-        if (act) {
-            cand = gt16_decode(T16[h], gt_code_of(F, h), g);
-            if (cand < 0 || p - cand < 1 || p - cand > 65535) cand = -1;
-        }
-#else
-        if (act) {
-            const int32_t ov = T[h];
-            cand = ov - 1;
-            if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
-        }
-#endif
-        const uint32_t vw = cand >= 0 ? ld_u32(j, cand) : 0u;
-        const uint64_t hm = __ballot(cand >= 0 && vw == seq);
-        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
-#if LZ4MI_GT16
-        if (lane < nprobe) {                                   // the probes that happen insert their position
-            T16[h] = (uint16_t)(p & 0x7FFF);
-            const uint32_t sh = (h & 15) * 2;                  // distinct hashes, maybe one code word: LDS atomics
-            atomicAnd(&F.code[h >> 4], ~(3u << sh));
-            atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
-        }
-#else
-        if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
-#endif
-        wait_vmem();                                           // ... before the next table access
-        if (!hm) {
-            i = lane_val(p + (int32_t)step, nb - 1);
-            c += nb;
-            continue;
-        }
-        const int m = nprobe - 1;
-        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
-        c = 67;
-        const int32_t e = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
-        pv = true;
-        p_anchor = anchor;
-        p_pm = pm;
-        p_off = (uint32_t)(pm - cm);
-        p_mcode = e - pm - 4;
-        i = e;
-        anchor = e;
-    }
-    if (pv) emit_seq(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode);
-    o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
-    ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
-    return o.op;
-}
 
 // ---------------------------------------------------------------------------
 // Speculative hit chains (round 3, default). After a hit of step S (match end -
 // probe position) the next probe is at the match end, and on mid-ratio data the
 // next match often has the same step again (tiles216: 94 % of matches are 64
-// bytes and followed directly by a hit). compress_block_gt spends two dependent
+// bytes and followed directly by a hit). One probe per step costs two dependent
 // global round trips per sequence (table, then the candidate's bytes); here one
 // batch probes up to kSpecK positions i, i + S, i + 2S, ... at once, assuming each
 // is a hit of step S:
@@ -1036,9 +644,6 @@ __device__ int64_t compress_block_gt(const CompJob& j, GtShared& F, int32_t* T, 
 // Round trips per sequence: 2 / (accepted probes per batch); tiles216 3.8 (CPU model
 // of the serial parse, K = 8). Table reads after the previous batch's stores need no
 // wait: one wave's load of an address it stored to observes the store (program order).
-#ifndef LZ4MI_GTSPEC
-#define LZ4MI_GTSPEC 1
-#endif
 constexpr int kSpecK = 8;     // probes per speculative batch (8 lanes each for the windows)
 constexpr int kSpecW = 128;   // window bytes per probe
 
@@ -1400,22 +1005,6 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, i
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
 }
 
-__global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, int32_t* tables) {
-    __shared__ GtShared F;
-    const uint32_t b = blockIdx.x;
-    if (b >= a.nblocks) return;
-    CompJob j;
-    j.src = a.in + a.in_off[b];
-    j.src_total = a.in_len[b];
-    j.start = 0;
-    j.len = (int32_t)a.in_len[b];
-    j.dst = a.out + a.out_off[b];
-    j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
-    j.dst_pos = 0;
-    j.table = nullptr;
-    const int64_t r = compress_block_gt(j, F, tables + (size_t)b * 16384, threadIdx.x);
-    if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
-}
 
 // ---------------------------------------------------------------------------
 // Dependent blocks (the reference's LZ4.compress default, bufferCompress.js:182-236): the
@@ -1424,170 +1013,15 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gt_kernel(CompArgs a, in
 // block's output in its own slot. One wave walks the whole chain, so everything it touches
 // is in LDS: the table (64 KiB, int32 as the reference's), the last 64 KiB of source plus up
 // to 24 KiB ahead (the ring above), the output ring; the probes of a miss chain go as one
-// 64-wide batch as in compress_block_gt. A sequence costs LDS round trips only (the batch
+// 64-wide batch as in compress_block_gts. A sequence costs LDS round trips only (the batch
 // encoder's two dependent global round trips per sequence, the old single-wave table kernel's
 // one probe per step, are what made dependent frames 0.027 GB/s).
 struct ChainShared {
-    uint8_t ring[kRing];
+    uint8_t ring[4096];   // output ring
     uint8_t slot[1024];   // batch duplicate-hash detection: lane ids keyed by hash & 1023
 };
 __shared__ int32_t g_ctab[16384];
 
-__device__ int64_t compress_block_chain(const CompJob& j, ChainShared& F, int lane, Ring& r) {
-    int32_t* T = g_ctab;
-    const int32_t start = j.start, end = j.start + j.len;
-    const int32_t mflimit = end - 12, matchlimit = end - 5;
-    FastOut o{j.dst, 0, 0};
-    int32_t i = start, anchor = start;
-    uint32_t c = 67;
-    int32_t wb = -(1 << 30);     // 256-byte source window [wb, wb+256): lane l holds bytes wb+4l..+3
-    uint32_t wl = 0;
-    bool pv = false;             // the previous match, emitted after the next probe's reads are issued
-    int32_t p_anchor = 0, p_pm = 0, p_mcode = 0;
-    uint32_t p_off = 0;
-#if LZ4MI_CPROFILE
-    uint64_t cprof[10] = {0};
-    uint64_t cprof_t = wall_clock64();
-#endif
-    while (i < mflimit) {
-        if (r.hi - i < kRingAhead) ring_advance(j, r, lane, i);
-        CPROF(6);
-        // ---- the probe at i: read and replace, then verification + speculative extension window
-        const int64_t off0 = (int64_t)i - wb;   // positions are absolute: up to 2^31
-        uint32_t seq0;
-        if (off0 >= 0 && off0 + 4 <= 4 * kWave) {
-            const int wi = off0 >> 2;
-            seq0 = funnel(__builtin_amdgcn_readlane(wl, wi), __builtin_amdgcn_readlane(wl, wi < kWave - 1 ? wi + 1 : wi),
-                          (uint32_t)(off0 & 3));
-        } else {
-            seq0 = uniform(SrcR::u32(j, &r, i));
-        }
-        const uint32_t h0 = (seq0 * kP1) >> 18;
-        const int32_t old = T[h0];
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) T[h0] = i + 1;
-        int32_t cand0 = old - 1;
-        if (old <= 0 || cand0 == i || (uint32_t)(i - cand0) > 65535u) cand0 = -1;
-        CPROF(0);
-        CPROF_COUNT(8, 1);
-        uint32_t aw = 0, bw = 0;
-        bool hit0 = false;
-        if (cand0 >= 0) {
-            const uint32_t vw = SrcR::u32(j, &r, cand0);
-            aw = SrcR::u32(j, &r, (int64_t)i + 4 + 4 * lane);
-            bw = SrcR::u32(j, &r, (int64_t)cand0 + 4 + 4 * lane);
-            hit0 = uniform(vw) == seq0;
-        }
-        if (pv) {
-            emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
-            pv = false;
-        }
-        CPROF(1);
-        if (hit0) {
-            CPROF_COUNT(9, 1);
-            c = 67;
-            const int32_t lim = matchlimit - (i + 4);
-            const uint32_t x = aw ^ bw;
-            const uint64_t xm = __ballot(x != 0);
-            int32_t f;
-            if (xm) {
-                const int fl = __builtin_ctzll(xm);
-                f = 4 * fl + (__builtin_ctz((uint32_t)lane_val(x, fl)) >> 3);
-            } else {
-                f = lim > 4 * kWave ? 4 * kWave + (int32_t)match_extent(j, lane, i + 4 + 4 * kWave,
-                                                                        cand0 + 4 + 4 * kWave, lim - 4 * kWave)
-                                    : lim;
-            }
-            if (f > lim) f = lim;
-            wb = i + 4;
-            wl = aw;
-            const int32_t e = i + 4 + f;
-            pv = true;
-            p_anchor = anchor;
-            p_pm = i;
-            p_off = (uint32_t)(i - cand0);
-            p_mcode = e - i - 4;
-            i = e;
-            anchor = e;
-            CPROF(3);
-            continue;
-        }
-        // ---- the probe at i missed (and inserted itself): the next probes of the miss chain as a batch
-        i += (int32_t)(c >> 6);
-        c += 1;
-        if (i >= mflimit) break;
-        const int32_t p = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
-        const uint32_t step = (c + lane) >> 6;
-        bool act = p < mflimit;
-        uint32_t seq = 0;
-        {
-            const int64_t off = (int64_t)p - wb;
-            const bool inw = off >= 0 && off + 4 <= 4 * kWave;
-            const int wi = inw ? (off >> 2) : 0;
-            const uint32_t w0 = __shfl(wl, wi, kWave), w1 = __shfl(wl, wi < kWave - 1 ? wi + 1 : wi, kWave);
-            seq = funnel(w0, w1, (uint32_t)(off & 3));
-            if (__ballot(act && !inw)) {
-                if (act && !inw) seq = SrcR::u32(j, &r, p);
-            }
-        }
-        const uint32_t h = (seq * kP1) >> 18;
-        {   // cut the batch before the first lane whose hash (mod 1024) repeats in it
-            volatile uint8_t* vs = F.slot;
-            if (act) vs[h & 1023] = (uint8_t)lane;
-            __builtin_amdgcn_wave_barrier();
-            const bool dup = act && vs[h & 1023] != (uint8_t)lane;
-            int nb = __popcll(__ballot(act));
-            const uint64_t dm = __ballot(dup);
-            if (dm) {
-                const int d = __builtin_ctzll(dm);
-                nb = d ? d : 1;
-            }
-            act = act && lane < nb;
-        }
-        const int nb = __popcll(__ballot(act));
-        int32_t cand = -1;
-        if (act) {
-            const int32_t ov = T[h];
-            cand = ov - 1;
-            if (ov <= 0 || cand == p || (uint32_t)(p - cand) > 65535u) cand = -1;
-        }
-        const uint32_t vw = cand >= 0 ? SrcR::u32(j, &r, cand) : 0u;
-        const uint64_t hm = __ballot(cand >= 0 && vw == seq);
-        const int nprobe = hm ? __builtin_ctzll(hm) + 1 : nb;
-        __builtin_amdgcn_wave_barrier();
-        if (lane < nprobe) T[h] = p + 1;                       // the probes that happen insert their position
-        __builtin_amdgcn_wave_barrier();
-        CPROF(2);
-        if (!hm) {
-            i = lane_val(p + (int32_t)step, nb - 1);
-            c += nb;
-            continue;
-        }
-        CPROF_COUNT(9, 1);
-        const int m = nprobe - 1;
-        const int32_t pm = lane_val(p, m), cm = lane_val(cand, m);
-        c = 67;
-        const int32_t e = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
-        pv = true;
-        p_anchor = anchor;
-        p_pm = pm;
-        p_off = (uint32_t)(pm - cm);
-        p_mcode = e - pm - 4;
-        i = e;
-        anchor = e;
-        CPROF(3);
-    }
-    if (pv) emit_seq<ChainShared, SrcR>(F, o, j, lane, p_anchor, p_pm, p_off, p_mcode, &r);
-    o = emit_tail<ChainShared, SrcR>(F, o, j, lane, anchor, end - anchor, &r);
-    ring_flush(F, o, lane);
-    for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];
-    CPROF(4);
-#if LZ4MI_CPROFILE
-    if (lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
-#endif
-    return o.op;
-}
 
 // The dependent-block chain with compress_block_gts's batching (round 3): hit batches of up to
 // kSpecK probes of one step, miss batches starting at the probe itself with the exact duplicate
@@ -1850,7 +1284,6 @@ struct ChainArgs {
     const uint64_t* out_off;
     uint32_t* comp_len;
     uint32_t nblocks;
-    int v1;               // 1: the one-sequence-per-step chain (A/B)
 };
 
 __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
@@ -1867,7 +1300,7 @@ __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
         const int32_t n = (int32_t)(rest < a.bsize ? rest : a.bsize);
         CompJob j{a.src, a.src_total, (int32_t)s0, n, a.out + a.out_off[b],
                   (uint64_t)n + (uint64_t)n / 255u + 16u, 0, nullptr};
-        const int64_t w = a.v1 ? compress_block_chain(j, F, lane, r) : compress_block_chain2(j, F, lane, r);
+        const int64_t w = compress_block_chain2(j, F, lane, r);
         if (lane == 0) a.comp_len[b] = (uint32_t)w;
     }
     __syncthreads();
@@ -1891,18 +1324,7 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
     lz4mi::CompArgs a{};
     a.in = in; a.in_off = in_off; a.in_len = in_len; a.out = out; a.out_off = out_off; a.out_len = out_len;
     a.nblocks = nblocks;
-    // encoder: LZ4MI_ENCODER=lds selects the LDS-table kernel (4 blocks per CU);
-    // default: global tables (16 blocks per CU; `tables` = 64 KiB per block of scratch)
-    const char* enc = getenv("LZ4MI_ENCODER");   // read per call: tools/compress_ab.py switches it in-process
-    if (enc && enc[0] == 'l') {
-        hipLaunchKernelGGL(lz4mi::lz4mi_compress_fast_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-        return hipGetLastError();
-    }
-    // LZ4MI_ENCODER=gt: the one-sequence-per-round-trip batch encoder (A/B against the default)
-    if (!LZ4MI_GTSPEC || (enc && enc[0] == 'g')) {
-        hipLaunchKernelGGL(lz4mi::lz4mi_compress_gt_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
-        return hipGetLastError();
-    }
+    // speculative hit-chain batch encoder, 16 blocks per CU; `tables` = per-block scratch
     hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
     return hipGetLastError();
 }
@@ -1922,9 +1344,7 @@ extern "C" hipError_t lz4mi_launch_compress_chain(const uint8_t* src, uint64_t s
                                                   int32_t bsize, int32_t* table, uint8_t* out, const uint64_t* out_off,
                                                   uint32_t* comp_len, uint32_t nblocks, hipStream_t stream) {
     if (nblocks == 0) return hipSuccess;
-    const char* v = getenv("LZ4MI_CHAIN");   // LZ4MI_CHAIN=v1: the one-sequence-per-step chain (A/B)
-    lz4mi::ChainArgs a{src, src_total, start, len, bsize, table, out, out_off, comp_len, nblocks,
-                       (v && v[0] == 'v' && v[1] == '1') ? 1 : 0};
+    lz4mi::ChainArgs a{src, src_total, start, len, bsize, table, out, out_off, comp_len, nblocks};
     hipLaunchKernelGGL(lz4mi::lz4mi_compress_chain_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
