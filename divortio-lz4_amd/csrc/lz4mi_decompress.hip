@@ -280,9 +280,12 @@ struct Run {
 
 __device__ __forceinline__ Run no_run() { return Run{0, 0, 0, 0, R_NONE}; }
 
+// lane l's value (l wave-uniform): v_readlane, not an LDS permute
+__device__ __forceinline__ int32_t lane_of(int32_t v, int l) { return (int32_t)__builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l); }
+
 __device__ __forceinline__ Run shfl_run(const Run& R, int l) {
-    return Run{__shfl(R.y, l, kWave), __shfl(R.n, l, kWave), __shfl(R.src, l, kWave), __shfl(R.period, l, kWave),
-               (uint32_t)__shfl((int)R.kind, l, kWave)};
+    return Run{lane_of(R.y, l), lane_of(R.n, l), lane_of(R.src, l), lane_of(R.period, l), lane_of(R.kind, l)};
 }
 
 // The match run of a sequence whose match starts at ms; n = 0 when nothing is
@@ -786,8 +789,8 @@ __device__ __forceinline__ int64_t wave_varint(const Ctx& c, int lane, int64_t& 
         uint64_t mask = __ballot(first < 16);
         if (mask) {
             int fl = __builtin_ctzll(mask);
-            int fi = __shfl(first, fl, kWave);
-            uint32_t fb = __shfl(lastb, fl, kWave);
+            int fi = lane_of(first, fl);
+            uint32_t fb = lane_of(lastb, fl);
             int64_t cnt = (int64_t)fl * 16 + fi;
             sum += 255 * cnt + fb;
             q += cnt + 1;
@@ -1016,7 +1019,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         }
         if (nE >= seg1) vis = 0;
         else vis &= ~((1u << (nE - seg0)) - 1u);
-        tail = uniform(__shfl(x, kWave - 1, kWave));   // where the chain leaves the chunk
+        tail = lane_of(x, kWave - 1);   // where the chain leaves the chunk
         }
         (void)seg1;
         const uint64_t has = __ballot(vis != 0);
@@ -1042,7 +1045,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         const uint32_t cnt = __popc(vis) - ((cut && lane == last_lane) ? 1u : 0u);
         const uint32_t incl = wave_incl_scan(cnt, lane);
         const uint32_t base = incl - cnt;
-        const uint32_t nseq = uniform(__shfl(incl, kWave - 1, kWave));
+        const uint32_t nseq = lane_of(incl, kWave - 1);
         uint32_t run = 0;
         {
             uint32_t m = vis, k = base;
@@ -1076,7 +1079,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         }
         const uint32_t lincl = wave_incl_scan(run, lane);
         const uint32_t lbase = lincl - run;
-        const int64_t total = uniform(__shfl(lincl, kWave - 1, kWave));
+        const int64_t total = lane_of(lincl, kWave - 1);
         uint32_t first_err = 0xFFFFFFFFu;
         for (uint32_t k = base; k < base + cnt; ++k) {
             const int64_t os = c.O + lbase + S.t_out[k];
