@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -89,7 +90,7 @@ struct StreamCtx {
 };
 
 struct Ctx {
-    int device = -1;
+    std::atomic<int> device{-1};   // set once by init_locked, never changed after
     hipStream_t stream = nullptr;
     Scratch in, out, meta, aux;   // staging of the synchronous host-pointer entry points
     std::mutex mu;                // serialises the host-pointer entry points (their staging is shared)
@@ -253,25 +254,9 @@ static int32_t init_locked(int32_t device) {
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return LZ4MI_ERR_HIP;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LZ4MI_ERR_NO_DEVICE;
     if (g_ctx.device == device) return LZ4MI_OK;
-    if (g_ctx.device >= 0) {
-        // switching devices: every buffer of the old context lives on the old device
-        std::lock_guard<std::mutex> lk2(g_ctx.mu);
-        LZ4MI_TRY(hipSetDevice(g_ctx.device));
-        LZ4MI_TRY(hipDeviceSynchronize());
-        g_ctx.in.release();
-        g_ctx.out.release();
-        g_ctx.meta.release();
-        g_ctx.aux.release();
-        g_ctx.stats.release();
-        {
-            std::lock_guard<std::mutex> lk3(g_ctx.streams_mu);
-            for (auto& c : g_ctx.streams) c->release();
-            g_ctx.streams.clear();
-        }
-        if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
-        g_ctx.stream = nullptr;
-        g_ctx.device = -1;
-    }
+    // the context is bound to one device for the life of the process: another thread may
+    // hold a StreamCtx* (and its lock) of this device, so nothing of it is ever released
+    if (g_ctx.device >= 0) return LZ4MI_ERR_ARG;
     LZ4MI_TRY(hipSetDevice(device));
     LZ4MI_TRY(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     g_ctx.device = device;

@@ -72,12 +72,34 @@ def header(block_size, independent=True, content_checksum=False, content_size=No
 
 
 class DeviceCodec:
-    """The GPU path: batch encoder + device frame records (one stream)."""
+    """The GPU path: batch encoder + device frame records (one stream). Its buffers are kept
+    for the next call of the same shape (allocation is not part of a frame's kernel time);
+    `last_kernel_s` is the encoder + record packing time from HIP events on the stream. The
+    returned records are a view of that workspace, valid until the next call."""
 
     def __init__(self, stream=None):
         import torch
         self.torch = torch
         self.stream = stream if stream is not None else torch.cuda.current_stream()
+        self.ws = None
+        self.last_kernel_s = None
+
+    def _workspace(self, nb, n, block_size, block_checksum, dev):
+        import lz4mi
+        torch = self.torch
+        key = (nb, n, block_size, block_checksum, str(dev))
+        if self.ws is None or self.ws["key"] != key:
+            self.ws = None
+            raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * block_size
+            raw_len = torch.clamp(n - raw_off, max=block_size).to(torch.int32)
+            slot = (lz4mi.compress_bound(block_size) + 255) & ~255
+            rec_max = int((4 + raw_len.to(torch.int64) + (4 if block_checksum else 0)).sum().item())
+            self.ws = {"key": key, "raw_off": raw_off, "raw_len": raw_len,
+                       "comp": torch.empty(nb * slot, dtype=torch.uint8, device=dev),
+                       "comp_off": torch.arange(nb, dtype=torch.int64, device=dev) * slot,
+                       "comp_len": torch.zeros(nb, dtype=torch.int32, device=dev),
+                       "out": torch.empty(max(1, rec_max), dtype=torch.uint8, device=dev)}
+        return self.ws
 
     def records(self, raw, block_size, block_checksum):
         """This rank's frame records (uint8 device tensor) for raw (uint8 device tensor)."""
@@ -86,27 +108,26 @@ class DeviceCodec:
         s = self.stream.cuda_stream
         n = raw.numel()
         nb = -(-n // block_size)
+        self.last_kernel_s = None
         if nb == 0:
             return torch.empty(0, dtype=torch.uint8, device=raw.device)
-        dev = raw.device
-        raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * block_size
-        raw_len = torch.clamp(n - raw_off, max=block_size).to(torch.int32)
-        slot = (lz4mi.compress_bound(block_size) + 255) & ~255
-        comp = torch.empty(nb * slot, dtype=torch.uint8, device=dev)
-        comp_off = torch.arange(nb, dtype=torch.int64, device=dev) * slot
-        comp_len = torch.zeros(nb, dtype=torch.int32, device=dev)
+        w = self._workspace(nb, n, block_size, block_checksum, raw.device)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self.stream):
-            lz4mi.compress_blocks_dev(raw.data_ptr(), raw_off.data_ptr(), raw_len.data_ptr(), comp.data_ptr(),
-                                      comp_off.data_ptr(), comp_len.data_ptr(), nb, s)
-            rec = shard.record_sizes(comp_len, raw_len) + (4 if block_checksum else 0)
+            e0.record(self.stream)
+            lz4mi.compress_blocks_dev(raw.data_ptr(), w["raw_off"].data_ptr(), w["raw_len"].data_ptr(),
+                                      w["comp"].data_ptr(), w["comp_off"].data_ptr(), w["comp_len"].data_ptr(), nb, s)
+            rec = shard.record_sizes(w["comp_len"], w["raw_len"]) + (4 if block_checksum else 0)
             rec_off = torch.cumsum(rec, 0) - rec
-            total = int(rec.sum().item())
-            out = torch.empty(total, dtype=torch.uint8, device=dev)
-            lz4mi.frame_pack_dev(raw.data_ptr(), raw_off.data_ptr(), raw_len.data_ptr(), comp.data_ptr(),
-                                 comp_off.data_ptr(), comp_len.data_ptr(), out.data_ptr(), rec_off.data_ptr(), nb, s,
-                                 block_checksum=block_checksum)
+            lz4mi.frame_pack_dev(raw.data_ptr(), w["raw_off"].data_ptr(), w["raw_len"].data_ptr(), w["comp"].data_ptr(),
+                                 w["comp_off"].data_ptr(), w["comp_len"].data_ptr(), w["out"].data_ptr(),
+                                 rec_off.data_ptr(), nb, s, block_checksum=block_checksum)
+            e1.record(self.stream)
         self.stream.synchronize()
-        return out
+        self.last_kernel_s = e0.elapsed_time(e1) / 1e3
+        total = int((rec_off[-1] + rec[-1]).item())
+        return w["out"][:total]
 
 
 class _ChecksumWorker:
@@ -207,88 +228,206 @@ def _host_pieces(t, piece=_STAGE_PIECE, nbuf=4):
         yield b.numpy()
 
 
-def staged_checksum(shard, group=None, root=0, seed=0):
-    """XXH32 (the reference's variant, 64-bit length) of every rank's shard concatenated in
-    rank order, computed on root's host: the content checksum is one serial chain,
-    so it runs on one core, but the bytes need not cross xGMI — the ranks share the host.
-    Each other rank copies its shard (1-D uint8 tensor, device or host) into a /dev/shm
-    segment; root hashes its own shard meanwhile (device-to-host piece by piece, the chain on
-    a worker thread), then each rank's segment in order. Returns the digest on root, None
-    elsewhere."""
-    import torch
-    dist, multi, world, rank = _dist_ctx(group)
-    n = shard.numel()
-    if not multi:
-        w = _ChecksumWorker(seed)
-        for a in _host_pieces(shard):
-            w.feed(a)
-        return w.digest()
-    dev = shard.device
-    t = torch.tensor([n], dtype=torch.int64, device=dev)
-    all_n = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(all_n, t, group=group)
-    sizes = [int(x.item()) for x in all_n]
-    # every rank must agree on the staging route before anyone writes: the segments of all
-    # non-root ranks must fit the shared memory filesystem (a memmap write past a full tmpfs
-    # is a SIGBUS, not an exception), else the shards go to root piece by piece over the group
-    need = sum(sizes[r] for r in range(world) if r != root)
-    ok = torch.tensor([1 if _shm_free() >= need + (1 << 30) else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-    if not int(ok.item()):
-        return _sent_checksum(shard, sizes, dist, group, world, rank, root, seed)
-    _stage_calls[0] += 1
-    tag = torch.tensor([os.getpid(), _stage_calls[0]], dtype=torch.int64, device=dev)
-    dist.broadcast(tag, src=dist.get_global_rank(group, root) if group is not None else root, group=group)
-    tag = [int(x) for x in tag.tolist()]
-    path = lambda r: os.path.join(_shm_dir(), f"lz4mi_stage_{tag[0]}_{tag[1]}_{r}.bin")
-    if rank != root:
+def _host_id():
+    """This host's identity as an int64 (host name + boot id): ranks whose ids match share a
+    /dev/shm, the precondition of the host-staged checksum route."""
+    import hashlib
+    import socket
+    boot = ""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        pass
+    h = hashlib.sha256((socket.gethostname() + "|" + boot).encode()).digest()
+    return int.from_bytes(h[:8], "little") & 0x7FFFFFFFFFFFFFFF
+
+
+class ContentChecksum:
+    """The frame's content checksum: XXH32 (the reference's variant, 64-bit length) of every
+    rank's shard concatenated in rank order, on root's host (one serial chain, so one
+    core). Three steps, so the chain can run beside other work:
+
+      ContentChecksum(n, dev, group, root)   collectives, main thread: shard sizes, whether
+                                             all ranks share root's host and /dev/shm has room
+      .start(shard)                          no collectives: a background thread; on root it
+                                             hashes root's shard (device-to-host through pinned
+                                             buffers on a side stream, the chain on a worker
+                                             thread), then each other rank's /dev/shm segment
+                                             as soon as that rank's done-marker appears; on the
+                                             other ranks it writes the shard into its segment
+      .finish()                              joins, then one all-reduce of a success flag, so a
+                                             failure on any rank raises on every rank
+
+    When the ranks do not share a host (or tmpfs lacks room: a memmap written past a full tmpfs
+    is a SIGBUS, not an exception), the shards go to root over the group in finish() instead
+    (_sent_checksum), which is not overlapped. Returns the digest on root, None elsewhere."""
+
+    POLL_S = 0.0005
+    DEADLINE_S = 900.0
+
+    def __init__(self, n, dev, group=None, root=0, seed=0):
+        import torch
+        self.dist, self.multi, self.world, self.rank = _dist_ctx(group)
+        self.group, self.root, self.seed, self.dev = group, root, seed, dev
+        self.n = n
+        self.error = None
+        self.digest = None
+        self.thread = None
+        self.elapsed = 0.0
+        self.route = "single"
+        if not self.multi:
+            self.sizes = [n]
+            return
+        dist = self.dist
+        mine = torch.tensor([n, _host_id()], dtype=torch.int64, device=dev)
+        allv = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(self.world)]
+        dist.all_gather(allv, mine, group=group)
+        allv = [[int(x) for x in v.tolist()] for v in allv]
+        self.sizes = [v[0] for v in allv]
+        same_host = all(v[1] == allv[0][1] for v in allv)
+        need = sum(self.sizes[r] for r in range(self.world) if r != root)
+        ok = torch.tensor([1 if same_host and _shm_free() >= need + (1 << 30) else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if not int(ok.item()):
+            self.route = "send"
+            return
+        self.route = "shm"
+        _stage_calls[0] += 1
+        tag = torch.tensor([os.getpid(), _stage_calls[0]], dtype=torch.int64, device=dev)
+        dist.broadcast(tag, src=self._g(root), group=group)
+        self.tag = [int(x) for x in tag.tolist()]
+
+    def _g(self, r):
+        return self.dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def _path(self, r, suffix=""):
+        return os.path.join(_shm_dir(), f"lz4mi_stage_{self.tag[0]}_{self.tag[1]}_{r}.bin{suffix}")
+
+    def start(self, shard):
+        self.shard = shard
+        if self.route == "send":
+            return self
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+        return self
+
+    def _run(self):
+        import time
+        import torch
+        t0 = time.perf_counter()
+        try:
+            ctx = torch.cuda.device(self.shard.device) if self.shard.device.type == "cuda" else None
+            side = torch.cuda.Stream(self.shard.device) if ctx is not None else None
+            if ctx is not None:
+                ctx.__enter__()
+            try:
+                if ctx is not None:
+                    with torch.cuda.stream(side):
+                        self._work()
+                else:
+                    self._work()
+            finally:
+                if ctx is not None:
+                    ctx.__exit__(None, None, None)
+        except BaseException as e:     # reported by finish() on every rank
+            self.error = e
+        self.elapsed = time.perf_counter() - t0
+
+    def _work(self):
+        import time
+        import torch
+        shard = self.shard
+        if self.route == "single" or self.rank == self.root:
+            w = _ChecksumWorker(self.seed)
+            try:
+                for r in range(self.world):
+                    if r == self.root or self.route == "single":
+                        for a in _host_pieces(shard):
+                            w.feed(a)
+                        continue
+                    deadline = time.perf_counter() + self.DEADLINE_S
+                    while not os.path.exists(self._path(r, ".done")):
+                        if os.path.exists(self._path(r, ".err")):
+                            raise RuntimeError(f"lz4mi: rank {r} failed to stage its shard for the content checksum")
+                        if time.perf_counter() > deadline:
+                            raise TimeoutError(f"lz4mi: rank {r} did not stage its shard for the content checksum")
+                        time.sleep(self.POLL_S)
+                    if self.sizes[r]:
+                        mm = np.memmap(self._path(r), dtype=np.uint8, mode="r", shape=(self.sizes[r],))
+                        for p in range(0, self.sizes[r], _STAGE_PIECE):
+                            w.feed(mm[p:p + _STAGE_PIECE])
+                        del mm
+            finally:
+                self.digest = w.digest()
+            return
+        n = shard.numel()
         try:
             if n:
-                mm = np.memmap(path(rank), dtype=np.uint8, mode="w+", shape=(n,))
+                mm = np.memmap(self._path(self.rank), dtype=np.uint8, mode="w+", shape=(n,))
                 for p in range(0, n, _STAGE_PIECE):
                     m = min(_STAGE_PIECE, n - p)
                     torch.from_numpy(mm[p:p + m]).copy_(shard[p:p + m])
                 mm.flush()
                 del mm
-            dist.barrier(group=group)       # staged
-            dist.barrier(group=group)       # root has read it
+            marker = ".done"
+        except BaseException:
+            if os.path.exists(self._path(self.rank)):
+                os.unlink(self._path(self.rank))
+            marker = ".err"
+            raise
         finally:
-            if os.path.exists(path(rank)):
-                os.unlink(path(rank))
-        return None
-    w = _ChecksumWorker(seed)
-    staged = False
-    for r in range(world):
-        if r == root:
-            for a in _host_pieces(shard):
-                w.feed(a)
-            continue
-        if not staged:
-            dist.barrier(group=group)
-            staged = True
-        if sizes[r]:
-            mm = np.memmap(path(r), dtype=np.uint8, mode="r", shape=(sizes[r],))
-            for p in range(0, sizes[r], _STAGE_PIECE):
-                w.feed(mm[p:p + _STAGE_PIECE])
-    d = w.digest()
-    if not staged:
-        dist.barrier(group=group)
-    dist.barrier(group=group)
-    return d
+            tmp = self._path(self.rank, marker + ".tmp")
+            with open(tmp, "w") as f:
+                f.write(marker)
+            os.rename(tmp, self._path(self.rank, marker))
+
+    def finish(self):
+        """Join the background chain; raises on every rank if any rank failed. Returns the
+        digest on root (None elsewhere)."""
+        import torch
+        if self.route == "send":
+            return _sent_checksum(self.shard, self.sizes, self.dist, self.group, self.world, self.rank, self.root,
+                                  self.seed)
+        if self.thread is not None:
+            self.thread.join()
+        if self.multi:
+            ok = torch.tensor([0 if self.error is not None else 1], dtype=torch.int32, device=self.dev)
+            self.dist.all_reduce(ok, op=self.dist.ReduceOp.MIN, group=self.group)
+            if self.rank == self.root:          # every rank is past its writes: remove what is left
+                for r in range(self.world):
+                    for suf in ("", ".done", ".err"):
+                        if os.path.exists(self._path(r, suf)):
+                            os.unlink(self._path(r, suf))
+            if not int(ok.item()):
+                raise self.error if self.error is not None else RuntimeError(
+                    "lz4mi: the content checksum failed on another rank")
+        elif self.error is not None:
+            raise self.error
+        return self.digest if (self.rank == self.root or not self.multi) else None
 
 
-def _phase(timings, key, t0, dev):
-    """Close a timed phase: device work done, all ranks through it (barrier)."""
+def staged_checksum(shard, group=None, root=0, seed=0):
+    """XXH32 (the reference's variant, 64-bit length) of every rank's shard concatenated in
+    rank order, on root's host (ContentChecksum, run to completion). Returns the digest on
+    root, None elsewhere."""
+    return ContentChecksum(shard.numel(), shard.device, group, root, seed).start(shard).finish()
+
+
+def _phase(timings, key, t0, dev, group=None):
+    """Close a timed phase: device work done, all ranks of `group` through it (barrier). Without
+    `timings` nothing is synchronised."""
     import time
     import torch
     import torch.distributed as dist
+    if timings is None:
+        return t0
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     if dist.is_available() and dist.is_initialized():
-        dist.barrier()
+        dist.barrier(group=group)
     t = time.perf_counter()
-    if timings is not None:
-        timings[key] = timings.get(key, 0.0) + (t - t0)
+    timings[key] = timings.get(key, 0.0) + (t - t0)
     return t
 
 
@@ -321,15 +460,22 @@ def compress_frame_sharded(raw, block_size=4194304, content_checksum=True, add_c
     for r in range(world - 1):
         if sizes[r] % block_size:
             raise ValueError("lz4mi: every shard but the last must hold whole blocks")
-    t0 = _phase(timings, "setup", t0, dev)
+    # the content checksum reads only the raw input: its chain starts now, beside the
+    # kernel and the collective (bufferCompress.js:244-252 hashes the same bytes at the end)
+    ck = ContentChecksum(n, dev, group, root).start(raw) if content_checksum else None
+    t0 = _phase(timings, "setup", t0, dev, group)
     records = codec.records(raw, block_size, block_checksum)
-    t0 = _phase(timings, "kernel", t0, dev)
+    if timings is not None and getattr(codec, "last_kernel_s", None) is not None:
+        timings["kernel_device"] = timings.get("kernel_device", 0.0) + codec.last_kernel_s
+    t0 = _phase(timings, "kernel", t0, dev, group)
     body = shard.gather_records_to_root(records, root=root, group=group) if multi else records
-    t0 = _phase(timings, "collective", t0, dev)
-    csum = staged_checksum(raw, group, root) if content_checksum else None
-    t0 = _phase(timings, "checksum", t0, dev)
+    t0 = _phase(timings, "collective", t0, dev, group)
+    csum = ck.finish() if ck is not None else None
+    if timings is not None and ck is not None:
+        timings["checksum_chain"] = timings.get("checksum_chain", 0.0) + ck.elapsed
+    t0 = _phase(timings, "checksum_wait", t0, dev, group)
     if rank != root:
-        _phase(timings, "assemble", t0, dev)
+        _phase(timings, "assemble", t0, dev, group)
         return None
     total = sum(sizes)
     hdr = header(block_size, True, content_checksum, total if add_content_size else None, None, block_checksum)
@@ -338,7 +484,7 @@ def compress_frame_sharded(raw, block_size=4194304, content_checksum=True, add_c
     out[:len(hdr)] = torch.frombuffer(bytearray(hdr), dtype=torch.uint8).to(dev)
     out[len(hdr):len(hdr) + body.numel()] = body
     out[len(hdr) + body.numel():] = torch.frombuffer(bytearray(tail), dtype=torch.uint8).to(dev)
-    _phase(timings, "assemble", t0, dev)
+    _phase(timings, "assemble", t0, dev, group)
     return out
 
 
@@ -365,25 +511,39 @@ def frame_index(frame):
         meta = {"flg": int(h[1]), "content_size": int(h[2]), "block_max": int(h[6]), "end": int(h[5]),
                 "overflow": int(h[7])}
         return meta, pay[:nb], word[:nb].to(torch.int64) & 0xFFFFFFFF
-    info, blocks = shard.frame_blocks(frame.numpy())
+    import lz4mi
+    f = frame.numpy()
+    try:
+        info, blocks = shard.frame_blocks(f)
+    except ValueError:
+        raise lz4mi.Lz4miError(lz4mi.ERR_MAGIC)
+    if ((info["flg"] & 0xC0) >> 6) != 1:
+        raise lz4mi.Lz4miError(lz4mi.ERR_VERSION)
     pay = torch.tensor([p for p, _, _ in blocks], dtype=torch.int64)
     word = torch.tensor([(nb | (0x80000000 if st else 0)) for _, nb, st in blocks], dtype=torch.int64)
+    # as lz4mi_frame_index_kernel: the walk ran past the frame's end (a payload, its block
+    # checksum or the EndMark missing): the blocks cannot be cut out of it
     meta = {"flg": info["flg"], "content_size": info["content_size"], "block_max": info["block_max"],
-            "end": info["end"], "overflow": 0}
+            "end": info["end"], "overflow": int(info["end"] > f.size)}
     return meta, pay, word
 
 
 class DeviceDecoder:
     """The GPU path of a rank's share of a frame: one batched decode of its compressed
-    blocks (lz4mi_decompress_blocks, device pointers), stored blocks copied."""
+    blocks (lz4mi_decompress_blocks, device pointers), stored blocks copied. The output
+    buffer is kept for the next call of the same shape; `last_kernel_s` is the decode
+    launch's time from HIP events on the stream."""
 
     def __init__(self, stream=None):
         self.stream = stream
+        self.ws = None
+        self.last_kernel_s = None
 
     def decode(self, rng, pay_rel, word, block_max, last_cap):
         """rng: this rank's frame bytes (device); pay_rel/word: its blocks' payload positions in
         rng and size words (int64 tensors). Returns (output, statuses): output = the blocks'
-        decoded bytes concatenated in order; status 0 or the reference's error code."""
+        decoded bytes concatenated in order; status 0 or the reference's error code. The output
+        is a view of the decoder's workspace, valid until the next call."""
         import torch
         import lz4mi
         if rng.device.type != "cuda":          # a host frame: its bytes go to the current GPU once
@@ -392,13 +552,18 @@ class DeviceDecoder:
         dev = rng.device
         nb = pay_rel.numel()
         s = self.stream if self.stream is not None else torch.cuda.current_stream(dev)
+        self.last_kernel_s = None
         size = word & 0x7FFFFFFF
         stored = (word & 0x80000000) != 0
         cap = torch.full((nb,), block_max, dtype=torch.int64, device=dev)
         if nb:
             cap[-1] = last_cap
         slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * block_max
-        out = torch.empty(max(1, nb * block_max), dtype=torch.uint8, device=dev)
+        key = (nb, block_max, str(dev))
+        if self.ws is None or self.ws[0] != key:
+            self.ws = None
+            self.ws = (key, torch.empty(max(1, nb * block_max), dtype=torch.uint8, device=dev))
+        out = self.ws[1]
         status = torch.zeros(nb, dtype=torch.int32, device=dev)
         out_len = torch.zeros(nb, dtype=torch.int32, device=dev)
         ci = torch.nonzero(~stored).flatten()
@@ -409,12 +574,18 @@ class DeviceDecoder:
             c_cap = cap[ci].to(torch.int32).contiguous()
             c_len = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
             c_st = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
             with torch.cuda.stream(s):
+                e0.record(s)
                 lz4mi.decompress_blocks_dev(rng.data_ptr(), c_in_off.data_ptr(), c_in_len.data_ptr(), out.data_ptr(),
                                             c_out_off.data_ptr(), c_cap.data_ptr(), c_len.data_ptr(), c_st.data_ptr(),
                                             ci.numel(), s.cuda_stream)
+                e1.record(s)
                 out_len[ci] = c_len
                 status[ci] = c_st
+            s.synchronize()
+            self.last_kernel_s = e0.elapsed_time(e1) / 1e3
         for b in torch.nonzero(stored).flatten().tolist():      # stored blocks (rare): plain copies
             p, m = int(pay_rel[b]), int(size[b])
             if m > int(cap[b]):
@@ -447,7 +618,9 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     host-staged shards. Returns root's output (uint8 tensor), None on the other ranks (their
     part with gather=False). The frame's first error in block order is raised on every rank
     with the reference's message. `decoder` replaces DeviceDecoder (CPU tests); `timings`
-    gets index / scatter / kernel / gather / checksum phases, each closed by a barrier.
+    gets index / scatter / kernel / gather / checksum_wait phases, each closed by a barrier,
+    plus kernel_device (the decoder's HIP-event time) and checksum_chain (the chain's own
+    duration: it runs beside the gather, so checksum_wait is what it adds).
     `device`: where this rank's tensors live (default: frame's device on root, else the
     backend's: CUDA for nccl, host for gloo)."""
     import time
@@ -468,16 +641,25 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     decoder = decoder or DeviceDecoder()
     src = dist.get_global_rank(group, root) if (multi and group is not None) else root
     t0 = time.perf_counter()
-    # ---- index on root, broadcast
+    # ---- index on root, broadcast (a malformed frame raises on every rank, not only on root)
+    status = 0
+    meta = None
     if rank == root:
-        meta, pay, word = frame_index(frame)
-        hdr = torch.tensor([pay.numel(), meta["flg"], meta["content_size"], meta["block_max"], meta["end"],
+        try:
+            meta, pay, word = frame_index(frame)
+        except lz4mi.Lz4miError as e:
+            status = e.status
+    if meta is not None:
+        hdr = torch.tensor([0, pay.numel(), meta["flg"], meta["content_size"], meta["block_max"], meta["end"],
                             meta["overflow"]], dtype=torch.int64, device=dev)
     else:
-        hdr = torch.zeros(6, dtype=torch.int64, device=dev)
+        hdr = torch.zeros(7, dtype=torch.int64, device=dev)
+        hdr[0] = status
     if multi:
         dist.broadcast(hdr, src=src, group=group)
-    nb, flg, csize, bmax, end, overflow = [int(x) for x in hdr.tolist()]
+    status, nb, flg, csize, bmax, end, overflow = [int(x) for x in hdr.tolist()]
+    if status:
+        raise lz4mi.Lz4miError(status)
     if overflow:
         raise lz4mi.Lz4miError(lz4mi.ERR_MALFORMED)
     if not flg & 0x20:
@@ -485,19 +667,22 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     if rank != root:
         pay = torch.zeros(nb, dtype=torch.int64, device=dev)
         word = torch.zeros(nb, dtype=torch.int64, device=dev)
+    else:
+        pay, word = pay.to(dev), word.to(dev)
     if multi and nb:
         dist.broadcast(pay, src=src, group=group)
         dist.broadcast(word, src=src, group=group)
-    t0 = _phase(timings, "index", t0, dev)
+    t0 = _phase(timings, "index", t0, dev, group)
     # ---- contiguous runs of blocks: rank r's frame bytes [a_r, b_r)
     bsum = 4 if flg & 0x10 else 0
     size = word & 0x7FFFFFFF
     runs = [shard.shard_range(nb, r, world) for r in range(world)]
+    pay_h, size_h = pay.tolist(), size.tolist()
 
     def span(lo, hi):
         if hi <= lo:
             return 0, 0
-        return int(pay[lo]), int(pay[hi - 1] + size[hi - 1]) + bsum
+        return int(pay_h[lo]), int(pay_h[hi - 1] + size_h[hi - 1]) + bsum
 
     lo, hi = runs[rank]
     a, b = span(lo, hi)
@@ -518,12 +703,14 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
                 dist.recv(rng, src=src, group=group)
     else:
         rng = frame[a:b]
-    t0 = _phase(timings, "scatter", t0, dev)
+    t0 = _phase(timings, "scatter", t0, dev, group)
     # ---- decode this rank's run
     # each block decodes into block_max bytes (a block's output position depends on the sizes
     # before it, which only the decode gives); the content size is checked on the sum below
     last_cap = bmax
     out, status = decoder.decode(rng, pay[lo:hi] - a, word[lo:hi], bmax, last_cap)
+    if timings is not None and getattr(decoder, "last_kernel_s", None) is not None:
+        timings["kernel_device"] = timings.get("kernel_device", 0.0) + decoder.last_kernel_s
     bad = torch.nonzero(status != 0).flatten()
     first = torch.tensor([lo + int(bad[0]) if bad.numel() else nb, int(status[bad[0]]) if bad.numel() else 0],
                          dtype=torch.int64, device=dev)
@@ -534,27 +721,36 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     total = torch.tensor([out.numel()], dtype=torch.int64, device=dev)
     if multi:
         dist.all_reduce(total, group=group)
-    t0 = _phase(timings, "kernel", t0, dev)
+    t0 = _phase(timings, "kernel", t0, dev, group)
     if int(first[0]) < nb:
         raise lz4mi.Lz4miError(int(first[1]))
     if csize > 0 and int(total.item()) != csize:
         raise lz4mi.Lz4miError(lz4mi.ERR_MALFORMED, "lz4mi: decoded size differs from the frame's content size")
-    # ---- content checksum from host-staged shards (before the gather: the shards are local)
+    # ---- content checksum (bufferDecompress.js:213-217) from the decoded shards, its chain on
+    # root's host beside the gather of the outputs to root (the chain reads each rank's shard
+    # where it was decoded: host-staged, nothing crosses xGMI for it)
+    ck = None
     if verify_checksum and flg & 0x04:
-        d = staged_checksum(out, group, root)
+        ck = ContentChecksum(out.numel(), dev, group, root).start(out)
+    got = None
+    if gather and multi:
+        got = shard.gather_records_to_root(out, root=root, group=group)
+        t0 = _phase(timings, "gather", t0, dev, group)
+    if ck is not None:
+        d = ck.finish()
+        if timings is not None:
+            timings["checksum_chain"] = timings.get("checksum_chain", 0.0) + ck.elapsed
         ok = torch.tensor([1], dtype=torch.int64, device=dev)
         if rank == root:
             want = int.from_bytes(frame[end:end + 4].cpu().numpy().tobytes(), "little")
             ok[0] = int(d == want)
         if multi:
             dist.broadcast(ok, src=src, group=group)
-        t0 = _phase(timings, "checksum", t0, dev)
+        t0 = _phase(timings, "checksum_wait", t0, dev, group)
         if not int(ok[0]):
             raise lz4mi.Lz4miError(lz4mi.ERR_CHECKSUM)
     if not gather or not multi:
         return out if (rank == root or not gather) else None
-    got = shard.gather_records_to_root(out, root=root, group=group)
-    _phase(timings, "gather", t0, dev)
     return got
 
 
@@ -569,6 +765,7 @@ def decompress_frame_device(frame, js_exact=False, verify_checksum=True, stream=
     first error."""
     import torch
     import lz4mi
+    # the library binds one device per process: a frame on another device raises ERR_ARG here
     lz4mi.init(frame.device.index if frame.device.index is not None else torch.cuda.current_device())
     s = stream if stream is not None else torch.cuda.current_stream(frame.device)
     head = frame[:19].cpu().numpy()

@@ -78,7 +78,8 @@ static inline uint64_t lz4mi_compress_bound(uint64_t n) { return n + n / 255u + 
 const char* lz4mi_status_message(int32_t status);
 
 /* Device selection / info. Returns LZ4MI_OK or LZ4MI_ERR_*. lz4mi_init(-1) keeps the
- * current device (or HIP's current one); another device releases every buffer of the old one. */
+ * current device (or HIP's current one). The library binds to one device per process (one
+ * process per GPU): asking for another device once initialised returns LZ4MI_ERR_ARG. */
 int32_t lz4mi_init(int32_t device);
 int32_t lz4mi_device_count(void);
 const char* lz4mi_version(void);

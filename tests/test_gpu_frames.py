@@ -58,7 +58,7 @@ def test_config4_complete_frame_64mib():
     tim = {}
     back = F.decompress_frame_sharded(ref, verify_checksum=True, timings=tim)   # host frame
     assert np.array_equal(back.cpu().numpy(), host)
-    assert {"index", "scatter", "kernel", "checksum"} <= set(tim)
+    assert {"index", "scatter", "kernel", "checksum_wait", "kernel_device"} <= set(tim)
     # the block index of a ragged frame (4 + 4 + 4 + 3 MiB)
     part = host[:5 * (3 << 20)]
     odd = O.compress_frame(part, None, BLOCK, True, True, True)
@@ -79,6 +79,29 @@ def test_config4_complete_frame_64mib():
     with pytest.raises(lz4mi.Lz4miError) as ei:
         F.decompress_frame_sharded(corrupt, verify_checksum=True)
     assert str(ei.value) == "LZ4: Content Checksum Error"
+
+
+def test_config0_frame_through_device_path(manifest):
+    """BASELINE configs[0], the reference benchmark's call (benchWorker.js:47-54,
+    LZ4.compress(1 MiB of i % 251, null, 4194304, true, false)): the device frame path writes
+    the reference's frame byte for byte and decodes it back; a truncated copy of the frame
+    (host and device) is the reference's Malformed Input, not a read past its end."""
+    from lz4mi import frame as F
+    (c,) = cases_of(manifest, "config0")
+    i = c["input"]
+    data = O.generate(i["gen"], i["seed"], i["n"])
+    want = golden_bytes(c["frame_file"])
+    got = F.compress_frame_sharded(torch.from_numpy(data.copy()).cuda(), c["block"], content_checksum=c["checksum"],
+                                   add_content_size=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert np.array_equal(F.decompress_frame_device(got).cpu().numpy(), data)
+    assert np.array_equal(F.decompress_frame_sharded(got).cpu().numpy(), data)
+    cut = want[:want.size - 100].copy()
+    for fr in (cut, torch.from_numpy(cut).cuda()):
+        with pytest.raises(lz4mi.Lz4miError) as ei:
+            F.decompress_frame_sharded(fr)
+        assert str(ei.value) == "LZ4: Malformed Input"
 
 
 def test_frame_with_block_checksums_matches_oracle():

@@ -254,6 +254,43 @@ def test_full_size_digest_manifest(manifest, kind):
     assert torch.equal(dec, raw)
 
 
+def test_bench_batch_decode_vs_oracle_hashes():
+    """The bench's whole headline batch (4096 x 4 MiB tiles216, seeds 1..4096, bench.py Batch):
+    generated, compressed and decoded on the GPU; every decoded block's XXH32 (GPU) equals the
+    oracle's XXH32 of the oracle's own generation of that block on the host — an independent
+    check of all 16 GiB of decoded bytes, not the GPU's hash of its own input."""
+    torch = pytest.importorskip("torch")
+    n, bs = 4096, 4 << 20
+    dev, s = "cuda", torch.cuda.current_stream().cuda_stream
+    raw = torch.empty(n * bs, dtype=torch.uint8, device=dev)
+    lz4mi.generate_blocks_dev(raw.data_ptr(), "tiles216", 1, bs, n, s)
+    slot = (lz4mi.compress_bound(bs) + 255) & ~255
+    comp = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    roff = torch.arange(n, dtype=torch.int64, device=dev) * bs
+    rlen = torch.full((n,), bs, dtype=torch.int32, device=dev)
+    coff = torch.arange(n, dtype=torch.int64, device=dev) * slot
+    clen = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.compress_blocks_dev(raw.data_ptr(), roff.data_ptr(), rlen.data_ptr(), comp.data_ptr(), coff.data_ptr(),
+                              clen.data_ptr(), n, s)
+    del raw                                          # the decode is checked against the host oracle only
+    dec = torch.zeros(n * bs, dtype=torch.uint8, device=dev)
+    dlen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.decompress_blocks_dev(comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), dec.data_ptr(), roff.data_ptr(),
+                                rlen.data_ptr(), dlen.data_ptr(), st.data_ptr(), n, s)
+    dh = torch.zeros(n, dtype=torch.int32, device=dev)
+    lz4mi.xxh32_blocks_dev(dec.data_ptr(), roff.data_ptr(), dlen.data_ptr(), dh.data_ptr(), n, 0, s)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all()) and bool((dlen == bs).all())
+    got = [int(x) & 0xFFFFFFFF for x in dh.cpu().tolist()]
+    del dec, comp
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(8) as ex:               # the oracle's C calls drop the GIL
+        want = list(ex.map(lambda b: O.xxh32(O.generate("tiles216", 1 + b, bs)), range(n)))
+    bad = [b for b in range(n) if got[b] != want[b]]
+    assert not bad, bad[:10]
+
+
 def test_frame_pack_matches_reference_frame():
     """Device-side frame records (lz4mi_frame_pack) == the reference frame's block records."""
     import torch

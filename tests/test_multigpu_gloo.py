@@ -136,7 +136,7 @@ def _frame_worker(rank, world, port, q):
             tim = {}
             got = F.compress_frame_sharded(mine, bsize, True, True, bcs, codec=_OracleCodec(), timings=tim)
             ref = O.compress_frame(data, None, bsize, True, True, True, block_checksum=bcs)
-            ok = all(k in tim for k in ("kernel", "collective", "checksum", "assemble"))
+            ok = all(k in tim for k in ("kernel", "collective", "checksum_wait", "checksum_chain", "assemble"))
             if rank == 0:
                 ok = ok and got is not None and np.array_equal(got.numpy(), ref)
             else:
@@ -145,7 +145,7 @@ def _frame_worker(rank, world, port, q):
             fr = torch.from_numpy(ref.copy()) if rank == 0 else None
             back = F.decompress_frame_sharded(fr, True, decoder=_OracleDecoder(), timings=tim)
             ok_back = (back is not None and np.array_equal(back.numpy(), data)) if rank == 0 else back is None
-            ok_back = ok_back and all(k in tim for k in ("index", "scatter", "kernel", "checksum", "gather"))
+            ok_back = ok_back and all(k in tim for k in ("index", "scatter", "kernel", "checksum_wait", "gather"))
             # a corrupted content checksum: the reference's error on every rank
             bad = ref.copy()
             bad[-1] ^= 0x5A
@@ -155,6 +155,16 @@ def _frame_worker(rank, world, port, q):
                 ok_back = False
             except Exception as e:
                 ok_back = ok_back and "Content Checksum Error" in str(e)
+            # a bad magic number and a truncated frame (a block payload running past the end): the
+            # reference's errors on every rank, found on root (no rank may hang in a collective)
+            for broken, want in ((np.concatenate([np.zeros(4, np.uint8), ref[4:]]), "Invalid Magic Number"),
+                                 (ref[:ref.size // 2].copy(), "Malformed Input")):
+                try:
+                    F.decompress_frame_sharded(torch.from_numpy(broken) if rank == 0 else None, True,
+                                               decoder=_OracleDecoder())
+                    ok_back = False
+                except Exception as e:
+                    ok_back = ok_back and want in str(e)
             # the host-staged content checksum alone == the oracle's XXH32 of the whole input
             d = F.staged_checksum(mine)
             ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
@@ -165,6 +175,14 @@ def _frame_worker(rank, world, port, q):
                 d = F.staged_checksum(mine)
             finally:
                 F._shm_free = real_free
+            ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
+            # ranks on different hosts (no shared /dev/shm): the same, over the group
+            real_id = F._host_id
+            F._host_id = lambda: 1000 + rank
+            try:
+                d = F.staged_checksum(mine)
+            finally:
+                F._host_id = real_id
             ok = ok and (d == O.xxh32(data) if rank == 0 else d is None)
             res.append((ok, ok_back))
         q.put((rank, res))

@@ -145,6 +145,21 @@ def test_frames_compress(manifest):
         assert st == 0 and back.tobytes() == bytes(np.frombuffer(bytes(data), dtype=np.uint8)), f
 
 
+def test_config0_frame(manifest):
+    """BASELINE configs[0], the reference benchmark's call (benchWorker.js:47-54):
+    LZ4.compress(1 MiB of i % 251, null, 4194304, true, false) — frame bytes and decode."""
+    (c,) = cases_of(manifest, "config0")
+    i = c["input"]
+    data = O.generate(i["gen"], i["seed"], i["n"])
+    assert np.array_equal(data, np.arange(i["n"]) % 251)
+    frame = O.compress_frame(data, None, c["block"], c["indep"], c["checksum"], True)
+    assert c["outbuf_equal"] and frame.size == c["frame_len"] == c["outbuf_len"]
+    assert np.array_equal(frame, golden_bytes(c["frame_file"]))
+    st, back = O.decompress_frame(frame, None, js_compat=True)
+    assert st == 0 and c["dec_equals_input"] and np.array_equal(back, data)
+    assert "%08x" % O.xxh32(back) == c["dec_xxh"]
+
+
 def test_frames_decode_reference_vectors(manifest):
     (g,) = cases_of(manifest, "frames")
     for c in g["decode"]:

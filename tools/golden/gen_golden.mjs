@@ -340,6 +340,22 @@ for (const [name, src, genSpec] of blockInputs) {
     manifest.cases.push({ kind: 'block_checksum_skip', cases });
 }
 
+// ---- 11. BASELINE configs[0]: the reference's benchmark call on 1 MiB of i % 251 ------
+{
+    // benchmark/src/base/benchWorker.js:47-54: LZ4.compress(x, null, 4194304, true, false) for
+    // decompress runs, the same with addContentSize and a preallocated output buffer for compress.
+    const x = gen('repetitive', 1, 1 << 20);
+    const f = compressBuffer(x, null, 4194304, true, false);
+    const shared = new Uint8Array(x.length + (x.length / 255 | 0) + 1024);
+    const f7 = compressBuffer(x, null, 4194304, true, false, true, shared);
+    const back = tryCall(() => decompressBuffer(f));
+    manifest.cases.push({ kind: 'config0', input: { gen: 'repetitive', seed: 1, n: x.length }, block: 4194304, indep: true,
+        checksum: false, frame_file: save(f, 'config0_frame'), frame_len: f.length, frame_xxh: hex(xxHash32(f)),
+        outbuf_len: f7.length, outbuf_equal: f7.length === f.length && f7.every((v, i) => v === f[i]),
+        dec_ok: back.ok, dec_len: back.ok ? back.value.length : null, dec_xxh: back.ok ? hex(xxHash32(back.value)) : null,
+        dec_equals_input: back.ok && back.value.length === x.length && back.value.every((v, i) => v === x[i]) });
+}
+
 fs.writeFileSync(path.join(OUT, 'manifest.json'), JSON.stringify(manifest, null, 1));
 console.log('wrote', manifest.cases.length, 'case groups to', OUT);
 }
