@@ -30,8 +30,6 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, con
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
                                               const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*, uint32_t,
                                               uint64_t*, uint64_t*, uint32_t*, hipStream_t);
-extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t*, uint64_t, int32_t, int32_t, int32_t*, uint8_t*,
-                                                  uint64_t, int32_t, int64_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress_chain(const uint8_t*, uint64_t, int32_t, int32_t, int32_t, int32_t*,
                                                   uint8_t*, const uint64_t*, uint32_t*, uint32_t, hipStream_t);
 extern "C" hipError_t lz4mi_launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*,
@@ -469,42 +467,27 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
 int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
                                    int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off, uint32_t flags,
                                    void* stream) {
-    DeviceGuard dg;
-    if (dg.status()) return dg.status();
-    if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table)
+    if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table || out_off < 0)
         return LZ4MI_ERR_ARG;
-    if (out_off < 0) return LZ4MI_ERR_ARG;
     if (flags & LZ4MI_DEVICE_PTRS) return LZ4MI_ERR_ARG;   // host-only entry point (see header)
-    std::lock_guard<std::mutex> lk(g_ctx.mu);
-    hipStream_t s = pick_stream(stream);
-    // Candidates never reach further back than 65535 bytes: stage only
-    // src[base, start+len) and shift table values by `base` (int32 wrap keeps
-    // untouched entries exact; shifted-out entries stay rejected).
-    int64_t base = std::max<int64_t>(0, (int64_t)src_start - 65536);
-    uint64_t sbytes = (uint64_t)src_start + src_len - base;
-    uint64_t obytes = out_total > (uint64_t)out_off ? out_total - (uint64_t)out_off : 0;
-    LZ4MI_TRY(g_ctx.in.ensure(sbytes + 64, s));
-    LZ4MI_TRY(g_ctx.out.ensure(obytes + 64, s));
-    LZ4MI_TRY(g_ctx.meta.ensure(16384 * 4 + 64, s));
-    std::vector<int32_t> t(16384);
-    for (int k = 0; k < 16384; ++k) t[k] = (int32_t)((uint32_t)table[k] - (uint32_t)base);
-    int32_t* d_table = g_ctx.meta.as<int32_t>();
-    int64_t* d_ret = (int64_t*)(d_table + 16384);
-    if (sbytes) LZ4MI_TRY(hipMemcpyAsync(g_ctx.in.p, src + base, sbytes, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(hipMemcpyAsync(d_table, t.data(), 16384 * 4, hipMemcpyHostToDevice, s));
-    LZ4MI_TRY(lz4mi_launch_compress_table(g_ctx.in.as<uint8_t>(), sbytes, (int32_t)(src_start - base), src_len,
-                                          d_table, g_ctx.out.as<uint8_t>(), obytes, 0, d_ret, s));
-    int64_t ret[2] = {0, 0};
-    LZ4MI_TRY(hipMemcpyAsync(ret, d_ret, 16, hipMemcpyDeviceToHost, s));
-    LZ4MI_TRY(hipMemcpyAsync(t.data(), d_table, 16384 * 4, hipMemcpyDeviceToHost, s));
-    LZ4MI_TRY(hipStreamSynchronize(s));
-    uint64_t n = std::min<uint64_t>((uint64_t)ret[0], obytes);
-    if (n) LZ4MI_TRY(hipMemcpy(out + out_off, g_ctx.out.p, n, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 16384; ++k) table[k] = (int32_t)((uint32_t)t[k] + (uint32_t)base);
-    // the reference threw a RangeError from output.set (blockCompress.js:100,198): the bytes and
-    // table entries written before it stay written
-    if (ret[1]) return LZ4MI_ERR_RANGE;
-    return ret[0];
+    {
+        DeviceGuard dg;   // no device: the call fails like every other block call
+        if (dg.status()) return dg.status();
+    }
+    // Room for the worst case: the GPU chain kernel (the dependent-frame kernel with one
+    // block: the caller's table in LDS). Otherwise the reference's output.set() may throw
+    // mid-block (blockCompress.js:100, :198) with the bytes and table entries written up to
+    // that point kept, and writes past the buffer vanish: the host encoder, which follows
+    // the reference store by store.
+    const uint64_t room = out_total > (uint64_t)out_off ? out_total - (uint64_t)out_off : 0;
+    if (src_len == 0 || room < lz4mi_compress_bound((uint64_t)src_len))
+        return lz4mi_host_compress_block(src, src_total, src_start, src_len, table, out, out_total, out_off);
+    const uint64_t off0 = (uint64_t)out_off;
+    uint32_t clen = 0;
+    const int32_t st = lz4mi_compress_chain(src, src_total, src_start, src_len, src_len, table, out, &off0, &clen, 0,
+                                            stream);
+    if (st) return st;
+    return (int64_t)clen;
 }
 
 int32_t lz4mi_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len, int32_t block_size,

@@ -5,14 +5,15 @@
 // (Math.imul(seq, 2654435761) >>> 18), read-and-replace the 16384-entry table
 // slot, verify distance (< 65536) and content, skip ahead by (miss++ >> 6) on a
 // miss, extend forward only, emit, continue at the match end. Every decision
-// depends on the previous one, so each block is one wave walking that chain;
-// the wave's 64 lanes do the byte work of every step in parallel:
-//   - a 128-byte window of the source at the probe position (2 bytes/lane),
-//   - the 128 candidate bytes fetched in the same round trip as the window,
-//   - verification + forward extension by ballot over 128 byte compares,
-//   - emission (token, 255-runs, literal copy by aligned dwords, offset).
-// The 64 KiB hash table lives in LDS (one table per block, as the reference's
-// module-global Int32Array(16384)).
+// depends on the previous one, so each block is one wave walking that chain
+// exactly; the wave's 64 lanes make each step wide (speculative probe batches,
+// 128-byte window compares, emission) instead of making the chain parallel.
+// Two kernels:
+//   lz4mi_compress_gts_kernel    independent blocks, one wave per block, 16 per CU
+//                                (global 15-bit tables + LDS epoch codes);
+//   lz4mi_compress_chain_kernel  dependent blocks / one block with the caller's
+//                                table (LZ4.compressRaw): one wave, the table, the
+//                                source window and the output ring in LDS.
 #include "lz4mi_common.h"
 
 #include <cstdlib>
@@ -55,61 +56,12 @@ struct CompArgs {
     const uint64_t* out_off;
     uint32_t* out_len;
     uint32_t nblocks;
-    CompJob single;       // used when nblocks == 0 (table mode)
-    int64_t* single_ret;
 };
 
 constexpr uint32_t kP1 = 2654435761u;
 
 __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
-}
-
-__device__ __forceinline__ void put_byte(const CompJob& j, int64_t p, uint32_t v) {
-    if (p >= 0 && (uint64_t)p < j.dst_total) j.dst[p] = (uint8_t)v;
-}
-
-// Byte k of a 128-byte window held as lanes (lo: bytes 0..63, hi: 64..127).
-__device__ __forceinline__ uint32_t win_byte(uint32_t lo, uint32_t hi, uint32_t k) {
-    return k < 64 ? __builtin_amdgcn_readlane(lo, k) : __builtin_amdgcn_readlane(hi, k - 64);
-}
-
-// dst[p, p+n) = v (wave-parallel).
-__device__ void wave_fill(const CompJob& j, int lane, int64_t p, int64_t n, uint32_t v) {
-    for (int64_t k = lane; k < n; k += kWave) put_byte(j, p + k, v);
-}
-
-// dst[d, d+n) = src[s, s+n) (wave-parallel, aligned dword stores where possible).
-__device__ void wave_copy(const CompJob& j, int lane, int64_t d, int64_t s, int64_t n) {
-    if (n <= 0) return;
-    uintptr_t da = (uintptr_t)(j.dst + d);
-    int64_t head = (int64_t)((4 - (da & 3)) & 3);
-    if (head > n) head = n;
-    if (lane < head) put_byte(j, d + lane, src_byte(j, s + lane));
-    d += head; s += head; n -= head;
-    int64_t nw = n >> 2;
-    const uintptr_t sa = (uintptr_t)(j.src + s);
-    const uint32_t sh = (uint32_t)(sa & 3);
-    const uint32_t* s0 = (const uint32_t*)(sa - sh);
-    const bool in_range = (uint64_t)(d + 4 * nw) <= j.dst_total;
-    for (int64_t w = lane; w < nw; w += kWave) {
-        int64_t last = s + 4 * w + 4 + (sh ? 4 : 0) - sh;   // one past the last source byte read
-        uint32_t v;
-        if (s + 4 * w - (int64_t)sh >= 0 && (uint64_t)last <= j.src_total) {
-            uint32_t d0 = s0[w], d1 = sh ? s0[w + 1] : 0u;
-            v = funnel(d0, d1, sh);
-        } else {
-            v = src_byte(j, s + 4 * w) | (src_byte(j, s + 4 * w + 1) << 8) | (src_byte(j, s + 4 * w + 2) << 16) |
-                (src_byte(j, s + 4 * w + 3) << 24);
-        }
-        if (in_range) {
-            *(uint32_t*)(j.dst + d + 4 * w) = v;
-        } else {
-            for (int b = 0; b < 4; ++b) put_byte(j, d + 4 * w + b, v >> (8 * b));
-        }
-    }
-    int64_t t = n & 3;
-    if (lane < t) put_byte(j, d + 4 * nw + lane, src_byte(j, s + 4 * nw + lane));
 }
 
 // Value of v in lane l, l uniform (a ballot's ctz, a lane count): v_readlane
@@ -229,183 +181,12 @@ __device__ int64_t match_extent(const CompJob& j, int lane, int64_t a, int64_t b
     return lim;
 }
 
-// Token + literal-length extension bytes + literals; returns the new output position.
-// A run of more than 64 literals is one output.set() in the reference (blockCompress.js:100,
-// :198), which throws a RangeError instead of writing when the run does not fit: `range`
-// is set and the position after the length bytes returned (what was written stays).
-__device__ int64_t emit_literals(const CompJob& j, int lane, int64_t op, int64_t anchor, int64_t lit,
-                                 uint32_t mnib, bool& range) {
-    uint32_t tok = (lit >= 15 ? 0xF0u : (uint32_t)lit << 4) | mnib;
-    const int64_t tok_pos = op;
-    if (lane == 0) put_byte(j, op, tok);
-    ++op;
-    if (lit >= 15) {
-        int64_t ext = lit - 15;
-        int64_t nff = ext / 255;
-        wave_fill(j, lane, op, nff, 255);
-        if (lane == 0) put_byte(j, op + nff, (uint32_t)(ext - 255 * nff));
-        op += nff + 1;
-    }
-    if (lit > 64 && (uint64_t)(op + lit) > j.dst_total) {
-        // the reference ORs the match-length nibble into the token after the literal copy
-        if (lane == 0) put_byte(j, tok_pos, 0xF0u);
-        range = true;
-        return op;
-    }
-    wave_copy(j, lane, op, anchor, lit);
-    return op + lit;
-}
-
 // A register whose load has been waited for: redefine it opaquely so the compiler's
 // wait insertion stops tracking it. Without this, the window bytes carried into the
 // next probe are waited for with vmcnt(0), which also waits for every store the
 // previous sequence's emission issued after them: a store round trip per sequence on
 // the chain (the loads themselves completed long before).
 __device__ __forceinline__ void settle32(uint32_t& v) { asm volatile("" : "+v"(v)); }
-
-__device__ int64_t compress_block_wave(const CompJob& j, int32_t* T, int lane, bool& range) {
-    const int64_t end = (int64_t)j.start + j.len;
-    const int64_t mflimit = end - 12;
-    const int64_t matchlimit = end - 5;
-    int64_t i = j.start, anchor = j.start, op = j.dst_pos;
-    uint32_t miss = 67;
-    // 128-byte source window [wi, wi+128): lane k holds bytes wi+k and wi+64+k
-#if LZ4MI_CPROFILE
-    uint64_t cprof[10] = {0};
-    uint64_t cprof_t = wall_clock64();
-#endif
-    int64_t wi = i;
-    uint32_t wlo = src_byte(j, wi + lane), whi = src_byte(j, wi + 64 + lane);
-
-    while (i < mflimit) {
-        if (i + 4 > wi + 128) {
-            wi = i;
-            wlo = src_byte(j, wi + lane);
-            whi = src_byte(j, wi + 64 + lane);
-        }
-        settle32(wlo);
-        settle32(whi);
-        uint32_t k0 = (uint32_t)(i - wi);
-        uint32_t seq = win_byte(wlo, whi, k0) | (win_byte(wlo, whi, k0 + 1) << 8) |
-                       (win_byte(wlo, whi, k0 + 2) << 16) | (win_byte(wlo, whi, k0 + 3) << 24);
-        uint32_t h = (seq * kP1) >> 18;
-        CPROF(0);
-        CPROF_COUNT(8, 1);
-        int32_t cand = T[h] - 1;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) T[h] = (int32_t)i + 1;
-        cand = __builtin_amdgcn_readfirstlane(cand);
-        if (cand < 0 || cand == i || ((uint32_t)(i - cand) >> 16) != 0) {
-            i += miss++ >> 6;
-            CPROF(1);
-            continue;
-        }
-        CPROF(1);
-        // fetch the candidate's 128 bytes and re-anchor the window at i, one round trip
-        wi = i;
-        wlo = src_byte(j, i + lane);
-        whi = src_byte(j, i + 64 + lane);
-        uint32_t clo = src_byte(j, (int64_t)cand + lane), chi = src_byte(j, (int64_t)cand + 64 + lane);
-        uint64_t neq_lo = __ballot(wlo != clo);
-        settle32(wlo);
-        if (neq_lo & 0xFull) {                    // the 4-byte content check failed
-            i += miss++ >> 6;
-            CPROF(2);
-            continue;
-        }
-        CPROF(2);
-        CPROF_COUNT(9, 1);
-        miss = 67;
-        // forward extension: e = i+4.. while e < matchlimit and bytes equal
-        int64_t lim = matchlimit - i;             // compare bytes k in [4, lim)
-        uint64_t neq_hi = __ballot(whi != chi);
-        settle32(whi);
-        int64_t e;
-        {
-            uint64_t m_lo = neq_lo & ~0xFull;
-            int64_t f = m_lo ? __builtin_ctzll(m_lo) : (neq_hi ? 64 + __builtin_ctzll(neq_hi) : 128);
-            if (f < 128 || lim <= 128) {
-                e = i + (f < lim ? f : lim);
-            } else {
-                // keep extending 128 bytes per step; past 512 bytes, 2 KiB per step (match_extent)
-                int64_t p = i + 128;
-                int64_t mp = (int64_t)cand + 128;
-                for (;;) {
-                    if (p >= i + 512) {
-                        e = p + match_extent(j, lane, p, mp, matchlimit - p);
-                        break;
-                    }
-                    uint32_t a0 = src_byte(j, p + lane), a1 = src_byte(j, p + 64 + lane);
-                    uint32_t b0 = src_byte(j, mp + lane), b1 = src_byte(j, mp + 64 + lane);
-                    uint64_t n0 = __ballot(a0 != b0), n1 = __ballot(a1 != b1);
-                    int64_t g = n0 ? __builtin_ctzll(n0) : (n1 ? 64 + __builtin_ctzll(n1) : 128);
-                    int64_t l2 = matchlimit - p;
-                    if (g < 128 || l2 <= 128) { e = p + (g < l2 ? g : l2); break; }
-                    p += 128;
-                    mp += 128;
-                }
-            }
-        }
-        CPROF(3);
-        int64_t mcode = e - i - 4;
-        int64_t lit = i - anchor;
-        op = emit_literals(j, lane, op, anchor, lit, mcode >= 15 ? 15u : (uint32_t)mcode, range);
-        if (range) return op - j.dst_pos;
-        uint32_t off = (uint32_t)(i - cand);
-        if (lane == 0) { put_byte(j, op, off & 255); put_byte(j, op + 1, (off >> 8) & 255); }
-        op += 2;
-        if (mcode >= 15) {
-            int64_t ext = mcode - 15;
-            int64_t nff = ext / 255;
-            wave_fill(j, lane, op, nff, 255);
-            if (lane == 0) put_byte(j, op + nff, (uint32_t)(ext - 255 * nff));
-            op += nff + 1;
-        }
-        i = e;
-        anchor = e;
-        CPROF(4);
-    }
-#if LZ4MI_CPROFILE
-    if (lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
-#endif
-    op = emit_literals(j, lane, op, anchor, end - anchor, 0, range);
-    return op - j.dst_pos;
-}
-
-__global__ __launch_bounds__(64) void lz4mi_compress_kernel(CompArgs a) {
-    __shared__ int32_t T[16384];
-    const int lane = threadIdx.x;
-    CompJob j;
-    if (a.nblocks == 0) {
-        j = a.single;
-    } else {
-        uint32_t b = blockIdx.x;
-        j.src = a.in + a.in_off[b];
-        j.src_total = a.in_len[b];
-        j.start = 0;
-        j.len = (int32_t)a.in_len[b];
-        j.dst = a.out + a.out_off[b];
-        j.dst_total = (uint64_t)a.in_len[b] + a.in_len[b] / 255u + 16u;
-        j.dst_pos = 0;
-        j.table = nullptr;
-    }
-    for (int k = lane; k < 16384; k += kWave) T[k] = j.table ? j.table[k] : 0;
-    __syncthreads();
-    bool range = false;
-    int64_t n = compress_block_wave(j, T, lane, range);
-    __syncthreads();
-    if (j.table)
-        for (int k = lane; k < 16384; k += kWave) j.table[k] = T[k];
-    if (lane == 0) {
-        if (a.nblocks == 0) {
-            a.single_ret[0] = n;
-            a.single_ret[1] = range ? 1 : 0;   // RangeError of output.set (the reference throws)
-        } else {
-            a.out_len[blockIdx.x] = (uint32_t)n;
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Batch encoder (fresh table per block): the same parse, 4 blocks per CU.
@@ -1326,17 +1107,6 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
     a.nblocks = nblocks;
     // speculative hit-chain batch encoder, 16 blocks per CU; `tables` = per-block scratch
     hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t lz4mi_launch_compress_table(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len,
-                                                  int32_t* table, uint8_t* dst, uint64_t dst_total, int32_t dst_pos,
-                                                  int64_t* ret, hipStream_t stream) {
-    lz4mi::CompArgs a{};
-    a.nblocks = 0;
-    a.single = lz4mi::CompJob{src, src_total, start, len, dst, dst_total, dst_pos, table};
-    a.single_ret = ret;
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -52,6 +52,10 @@
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
 #endif
 
+#ifndef LZ4MI_PIECES
+#define LZ4MI_PIECES 1   // ready matches copied piece-parallel (piece_pipe); 0: one lane per match (A/B switch)
+#endif
+
 #ifndef LZ4MI_PROFILE
 #define LZ4MI_PROFILE 0  // timing-only variant (tools/): per-phase wall-clock accumulation
 #endif
@@ -613,21 +617,113 @@ __device__ __forceinline__ bool any_lslot(const LSlot (&s)[NB]) {
     return m != 0;
 }
 
-template <int NB>
-__device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, LaneMatchGen& g) {
+template <int NB, class Gen>
+__device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, Gen& g) {
     LSlot s0[NB], s1[NB];
     uint4 a0[NB], a1[NB];
-    g.fill<NB>(s0);
+    g.template fill<NB>(s0);
     lane_load<NB>(c, s0, a0);
     for (;;) {
         if (!__ballot(any_lslot<NB>(s0))) break;
-        g.fill<NB>(s1);
+        g.template fill<NB>(s1);
         lane_load<NB>(c, s1, a1);
         lane_store<NB>(c, S, s0, a0);
         if (!__ballot(any_lslot<NB>(s1))) break;
-        g.fill<NB>(s0);
+        g.template fill<NB>(s0);
         lane_load<NB>(c, s0, a0);
         lane_store<NB>(c, S, s1, a1);
+    }
+}
+
+// Piece-parallel copy of a set of ready matches (sources complete, non-periodic,
+// 16 <= n <= kLaneBytes): every match is cut into 16-byte pieces (the last one
+// overlaps its predecessor) and the pieces of all matches are dealt to the lanes
+// in order, 64 per row, so one store instruction writes ~64 pieces of ~15
+// consecutive matches (4-5 adjacent lanes per match) instead of one piece of
+// each of 64 matches 64+ bytes apart, and no lane idles behind a longer match of
+// another lane. A match list (rank -> {y, src, n, first piece}) and a bitmap of
+// first pieces live in the pending-list LDS (free while a round writes); a lane
+// finds its piece's match as the number of first pieces at or below it.
+struct PEnt {
+    int32_t y, src, n, p0;
+};
+constexpr int kPieceRows = 32;                 // bitmap rows: 2 sequence rows x 64 matches x <= 16 pieces
+static_assert(2 * kWave * (kLaneBytes / 16) <= kPieceRows * kWave, "bitmap holds two sequence rows");
+static_assert(2 * kWave * sizeof(PEnt) + kPieceRows * 8 <= sizeof(uint32_t) * (kLim / 2 + kMaxSeq),
+              "match list and bitmap fit the pending list");
+
+struct PieceGen {
+    const PEnt* L;
+    const uint64_t* bm;
+    uint32_t P;        // pieces
+    uint32_t t;        // next row
+    int32_t rb;        // ranks before row t, minus one
+    int lane;
+    template <int NB>
+    __device__ __forceinline__ void fill(LSlot (&s)[NB]) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const uint32_t row = t + j;
+            const uint32_t p = 64u * row + (uint32_t)lane;
+            s[j] = LSlot{0, 0, 0u};
+            if (64u * row < P) {
+                const uint64_t w = bm[row];
+                const int32_t below = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(w >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)w, 0u));
+                const int32_t r = rb + below + (int32_t)((w >> lane) & 1u);
+                rb += __popcll(w);
+                if (p < P) {
+                    const PEnt e = L[r];
+                    const int32_t d0 = 16 * ((int32_t)p - e.p0);
+                    const int32_t d = d0 < e.n - 16 ? d0 : e.n - 16;
+                    s[j] = LSlot{e.y + d, e.src + d, 16u};
+                }
+            }
+        }
+        t += NB;
+    }
+};
+
+// The matches of sequences 64 i + lane for every bit i of `ready` (sources: S.t_rsrc
+// where `rbits` says so), two sequence rows per batch.
+__device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t ready, uint32_t rbits, int lane,
+                                           uint32_t nseq) {
+    PEnt* L = reinterpret_cast<PEnt*>(S.pme);
+    uint64_t* bm = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(S.pme) + 2 * kWave * sizeof(PEnt));
+    for (uint32_t i0 = 0; 64u * i0 < nseq; i0 += 2) {
+        if (__ballot(((ready >> i0) & 3u) != 0) == 0) continue;
+        if (lane < kPieceRows) bm[lane] = 0;
+        __syncthreads();
+        uint32_t P = 0, R = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t i = i0 + h;
+            const bool rd = (ready >> i) & 1u;
+            int32_t y = 0, src = 0, n = 0;
+            if (rd) {
+                const uint32_t k = 64u * i + (uint32_t)lane;
+                const SeqInfo q = seq_info(S, k);
+                const int32_t ms = (int32_t)S.t_out[k] + q.ll;
+                y = ms;
+                n = (ms + q.ml > c.cap ? c.cap : ms + q.ml) - ms;
+                src = (rbits >> i) & 1u ? S.t_rsrc[k] : ms - q.off;
+            }
+            const uint32_t np = rd ? (uint32_t)(n + 15) >> 4 : 0u;
+            const uint32_t incl = wave_incl_scan(np, lane);
+            const uint64_t bal = __ballot(rd);
+            const uint32_t r = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            const uint32_t p0 = P + incl - np;
+            if (rd) {
+                L[r] = PEnt{y, src, n, (int32_t)p0};
+                atomicOr((unsigned long long*)&bm[p0 >> 6], 1ull << (p0 & 63u));
+            }
+            P += lane_of(incl, kWave - 1);
+            R += (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+        PieceGen g{L, bm, P, 0u, -1, lane};
+        lane_pipe<kB>(c, S, g);
+        __syncthreads();   // the next batch rewrites the list
     }
 }
 
@@ -1217,10 +1313,14 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_round1(S));
             PROF(18);
         }
+#if LZ4MI_PIECES
+        piece_pipe(c, S, ready, rbits, lane, nseq);
+#else
         {
             LaneMatchGen g{c, S, ready, rbits, lane, 0, 0, 0, 0, 0};
             lane_pipe<kB>(c, S, g);
         }
+#endif
         PROF(19);
         for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
             uint32_t np = 0;
@@ -1268,10 +1368,14 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_rounds(S));
             }
+#if LZ4MI_PIECES
+            piece_pipe(c, S, ready, 0u, lane, nseq);
+#else
             {
                 LaneMatchGen g{c, S, ready, 0u, lane, 0, 0, 0, 0, 0};
                 lane_pipe<kB>(c, S, g);
             }
+#endif
             __syncthreads();
         }
         PROF(6);

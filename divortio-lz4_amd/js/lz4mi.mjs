@@ -13,8 +13,14 @@
  * greedy parse; the decoder runs the LZ4-spec kernel and re-decodes, with the
  * serial reference-exact kernel, any block where the reference's
  * double-copy-tail rewrite (SURVEY.md F1) would change a byte (flag JS_EXACT).
+ *
+ * Routing (SURVEY.md §8b): independent blocks go to the GPU in batches; work that is
+ * one serial chain by definition — dependent-block frames (LZ4.compress's default,
+ * bufferCompress.js:182-236) and a dictionary frame's first block — runs on the
+ * addon's host encoder (csrc/lz4mi_host.cpp), byte-identical, because one GPU wave
+ * walks a chain ~10x slower than one CPU core (DESIGN §4.2, §5 "Routing").
  * There is no CPU fallback: without the addon or a gfx950 device every call
- * throws.
+ * throws, the host-routed ones included.
  */
 import { createRequire } from 'module';
 
@@ -30,6 +36,15 @@ const DECODE_BATCH_BYTES = 256 * 1024 * 1024;   // output slots per batched deco
 // module-global table, as the reference's GLOBAL_HASH_TABLE (bufferCompress.js:56)
 const HASH_TABLE = new Int32Array(HASH_TABLE_SIZE);
 let decodeFlags = native.JS_EXACT;
+let deviceChecked = false;
+
+// The host-routed calls still require the device the library serves (no CPU fallback).
+function requireDevice() {
+    if (deviceChecked) return;
+    const st = native.deviceCount() === 0 ? -102 : native.init(-1);
+    if (st !== 0) throw new Error(native.statusMessage(st));
+    deviceChecked = true;
+}
 
 /** Coerce like the reference's ensureBuffer (src/shared/lz4Util.js:13-35). */
 export function ensureBuffer(input) {
@@ -203,7 +218,8 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
         if (dictLen > 0 && pos < end) {
             const n = Math.min(bsize, end - pos);
             const scratch = new Uint8Array(n + ((n / 255) | 0) + 16);
-            const c = native.compressBlock(work, scratch, pos, n, table, 0);
+            requireDevice();
+            const c = native.compressBlockHost(work, scratch, pos, n, table, 0);     // one chain: host route
             emit(pos, n, c, scratch.subarray(0, Math.max(0, Math.min(c, scratch.length))));
             table.fill(0);
             pos += n;
@@ -226,9 +242,10 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
             pos = end;
         }
     } else {
-        // Dependent blocks (the reference's default): one table carried across blocks, the
-        // whole chain in one GPU call (each block exactly compressBlock(work, scratch, pos, n,
-        // table, 0), the table updated in place).
+        // Dependent blocks (the reference's default): one table carried across blocks, each
+        // block exactly compressBlock(work, scratch, pos, n, table, 0), the table updated in
+        // place — one serial chain, so the host route (compressChain would run it as one GPU
+        // wave: 0.12 GB/s on tiles216 against ~1.5 GB/s for the host encoder, DESIGN §5).
         const nb = Math.ceil((end - pos) / bsize);
         if (nb > 0) {
             const outOff = new Float64Array(nb), compLen = new Uint32Array(nb);
@@ -239,7 +256,8 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
                 slot += n + ((n / 255) | 0) + 16;
             }
             const scratch = new Uint8Array(slot);
-            native.compressChain(work, pos, end - pos, bsize, table, scratch, outOff, compLen);
+            requireDevice();
+            native.compressChainHost(work, pos, end - pos, bsize, table, scratch, outOff, compLen);
             for (let b = 0; b < nb; b++) {
                 const n = Math.min(bsize, end - pos);
                 emit(pos, n, compLen[b], scratch.subarray(outOff[b], outOff[b] + compLen[b]));

@@ -38,7 +38,8 @@ EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_ve
            "lz4mi_decompress_blocks", "lz4mi_compress_blocks", "lz4mi_compress_block_table",
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
            "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
-           "lz4mi_frame_decompress", "lz4mi_frame_index", "lz4mi_compress_chain")
+           "lz4mi_frame_decompress", "lz4mi_frame_index", "lz4mi_compress_chain",
+           "lz4mi_host_compress_block", "lz4mi_host_compress_chain")
 
 
 class Lz4miError(RuntimeError):
@@ -96,6 +97,12 @@ def lib():
         L.lz4mi_compress_chain.restype = ctypes.c_int32
         L.lz4mi_compress_chain.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
                                            _vp, _vp, _vp, ctypes.c_uint32, _vp]
+        L.lz4mi_host_compress_block.restype = ctypes.c_int64
+        L.lz4mi_host_compress_block.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
+                                                ctypes.c_uint64, ctypes.c_int32]
+        L.lz4mi_host_compress_chain.restype = ctypes.c_int32
+        L.lz4mi_host_compress_chain.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                _vp, _vp, _vp, _vp]
         L.lz4mi_frame_index.restype = ctypes.c_int32
         L.lz4mi_frame_index.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
@@ -206,10 +213,11 @@ def compress_raw(src, output, src_start, src_len, hash_table, output_offset):
     return 0 if output_offset is None else int(r)   # (dIndex - undefined) | 0 (blockCompress.js:232)
 
 
-def compress_chain(src, start, length, block_size, hash_table):
-    """Dependent blocks in order with one carried table (lz4mi_compress_chain): returns the
-    list of compressed blocks, each what compressBlock(src, scratch, start_b, n_b, table, 0)
-    writes; hash_table (int32[16384]) is updated in place."""
+def compress_chain(src, start, length, block_size, hash_table, host=False):
+    """Dependent blocks in order with one carried table (lz4mi_compress_chain, or with `host`
+    the host encoder lz4mi_host_compress_chain): returns the list of compressed blocks, each
+    what compressBlock(src, scratch, start_b, n_b, table, 0) writes; hash_table (int32[16384])
+    is updated in place."""
     s = _u8(src)
     assert hash_table.dtype == np.int32 and hash_table.size == 16384 and hash_table.flags.c_contiguous
     nb = -(-length // block_size) if length > 0 else 0
@@ -221,9 +229,26 @@ def compress_chain(src, start, length, block_size, hash_table):
     out_off[1:] = np.cumsum(bounds[:-1])
     out = np.zeros(int(bounds.sum()), dtype=np.uint8)
     comp_len = np.zeros(nb, dtype=np.uint32)
-    _check(lib().lz4mi_compress_chain(_p(s), s.size, start, length, block_size, hash_table.ctypes.data, _p(out),
-                                      _p(out_off), _p(comp_len), 0, None))
+    if host:
+        _check(lib().lz4mi_host_compress_chain(_p(s), s.size, start, length, block_size, hash_table.ctypes.data,
+                                               _p(out), _p(out_off), _p(comp_len)))
+    else:
+        _check(lib().lz4mi_compress_chain(_p(s), s.size, start, length, block_size, hash_table.ctypes.data,
+                                          _p(out), _p(out_off), _p(comp_len), 0, None))
     return [out[int(o):int(o) + int(n)].copy() for o, n in zip(out_off, comp_len)]
+
+
+def host_compress_raw(src, output, src_start, src_len, hash_table, output_offset):
+    """compressRaw on the host encoder (lz4mi_host_compress_block): the same contract as
+    compress_raw, no device involved."""
+    s = _u8(src)
+    assert hash_table.dtype == np.int32 and hash_table.size == 16384 and hash_table.flags.c_contiguous
+    assert output.dtype == np.uint8 and output.flags.c_contiguous
+    r = lib().lz4mi_host_compress_block(_p(s), s.size, src_start, src_len, hash_table.ctypes.data, _p(output),
+                                        output.size, output_offset or 0)
+    if r < 0:
+        raise Lz4miError(int(r))
+    return 0 if output_offset is None else int(r)
 
 
 def _dec_flags(js_compat, js_exact):

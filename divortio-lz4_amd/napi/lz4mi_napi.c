@@ -116,8 +116,9 @@ static int is_undefined(napi_env env, size_t argc, napi_value* argv, size_t i) {
     return t == napi_undefined;
 }
 
-/* compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset) */
-static napi_value n_compress_block(napi_env env, napi_callback_info info) {
+/* compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset): lz4mi_compress_block_table;
+ * compressBlockHost: the host encoder (lz4mi_host_compress_block) */
+static napi_value compress_block_impl(napi_env env, napi_callback_info info, int host) {
     size_t argc = 6;
     napi_value argv[6];
     CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
@@ -138,13 +139,20 @@ static napi_value n_compress_block(napi_env env, napi_callback_info info) {
         table = (int32_t*)calloc(16384, sizeof(int32_t));   /* the reference would fault on a missing table */
         if (!table) return throw_status(env, LZ4MI_ERR_ARG);
     }
-    int64_t r = lz4mi_compress_block_table((const uint8_t*)src.data, src.length, to_i32(start), to_i32(len), table,
-                                           (uint8_t*)out.data, out.length, to_i32(ooff), 0, NULL);
+    int64_t r = host ? lz4mi_host_compress_block((const uint8_t*)src.data, src.length, to_i32(start), to_i32(len), table,
+                                                 (uint8_t*)out.data, out.length, to_i32(ooff))
+                     : lz4mi_compress_block_table((const uint8_t*)src.data, src.length, to_i32(start), to_i32(len),
+                                                  table, (uint8_t*)out.data, out.length, to_i32(ooff), 0, NULL);
     if (!tab.data) free(table);
     if (r < 0) return throw_status(env, r);
     /* without outputOffset the reference returns (dIndex - undefined) | 0 == 0 (blockCompress.js:37,232) */
     if (is_undefined(env, argc, argv, 5)) return make_i64(env, 0);
     return make_i64(env, r);
+}
+
+static napi_value n_compress_block(napi_env env, napi_callback_info info) { return compress_block_impl(env, info, 0); }
+static napi_value n_compress_block_host(napi_env env, napi_callback_info info) {
+    return compress_block_impl(env, info, 1);
 }
 
 /* decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary) */
@@ -246,8 +254,9 @@ static napi_value n_compress_blocks(napi_env env, napi_callback_info info) {
 }
 
 /* compressChain(src, start, len, blockSize, hashTable, out, outOff, compLen) -> 0: the dependent
- * blocks of one frame in one GPU chain (lz4mi_compress_chain) */
-static napi_value n_compress_chain(napi_env env, napi_callback_info info) {
+ * blocks of one frame in one GPU chain (lz4mi_compress_chain); compressChainHost: the same on
+ * the host encoder (lz4mi_host_compress_chain, the JS layer's route for dependent frames) */
+static napi_value compress_chain_impl(napi_env env, napi_callback_info info, int host) {
     size_t argc = 8;
     napi_value argv[8];
     CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
@@ -279,11 +288,20 @@ static napi_value n_compress_chain(napi_env env, napi_callback_info info) {
             return throw_status(env, LZ4MI_ERR_ARG);
         }
     }
-    int32_t st = lz4mi_compress_chain((const uint8_t*)src.data, src.length, (int32_t)start, (int32_t)len, (int32_t)bs,
-                                      (int32_t*)tab.data, (uint8_t*)out.data, offs, (uint32_t*)clen.data, 0, NULL);
+    int32_t st = host ? lz4mi_host_compress_chain((const uint8_t*)src.data, src.length, (int32_t)start, (int32_t)len,
+                                                  (int32_t)bs, (int32_t*)tab.data, (uint8_t*)out.data, offs,
+                                                  (uint32_t*)clen.data)
+                      : lz4mi_compress_chain((const uint8_t*)src.data, src.length, (int32_t)start, (int32_t)len,
+                                             (int32_t)bs, (int32_t*)tab.data, (uint8_t*)out.data, offs,
+                                             (uint32_t*)clen.data, 0, NULL);
     free(offs);
     if (st) return throw_status(env, st);
     return make_i64(env, 0);
+}
+
+static napi_value n_compress_chain(napi_env env, napi_callback_info info) { return compress_chain_impl(env, info, 0); }
+static napi_value n_compress_chain_host(napi_env env, napi_callback_info info) {
+    return compress_chain_impl(env, info, 1);
 }
 
 /* decompressBlocks(input, inOff, inLen, output, outOff, outCap, outLen, status, dictionary?, flags?) -> status */
@@ -481,6 +499,8 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"decompressBlock", NULL, n_decompress_block, NULL, NULL, NULL, napi_default, NULL},
         {"compressBlocks", NULL, n_compress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"compressChain", NULL, n_compress_chain, NULL, NULL, NULL, napi_default, NULL},
+        {"compressBlockHost", NULL, n_compress_block_host, NULL, NULL, NULL, napi_default, NULL},
+        {"compressChainHost", NULL, n_compress_chain_host, NULL, NULL, NULL, napi_default, NULL},
         {"decompressBlocks", NULL, n_decompress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"xxHash32", NULL, n_xxh32, NULL, NULL, NULL, napi_default, NULL},
         {"xxh32Reset", NULL, n_xxh32_reset, NULL, NULL, NULL, napi_default, NULL},

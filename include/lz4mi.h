@@ -125,15 +125,18 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
                               uint32_t nblocks, uint32_t flags, void* stream);
 
 /*
- * Single raw-block COMPRESS with a caller-owned hash table (dependent blocks,
- * dictionary prewarm, LZ4.compressRaw with a non-empty table).
+ * Single raw-block COMPRESS with a caller-owned hash table (LZ4.compressRaw with any table).
  * Replaces: compressBlock src/block/blockCompress.js:31-233 with full semantics:
  * positions are absolute in src[0 .. src_total); the block is
  * src[src_start .. +src_len); `table` (16384 int32, values = position+1, <=0 empty)
  * is read and written back; output written at out[out_off ..) (out_total bytes
  * available in out; writes past it are dropped, as with a typed array).
+ * With room for lz4mi_compress_bound(src_len) bytes at out_off the block runs on the GPU
+ * (the dependent-chain kernel, one block, the table in LDS); with less, the reference's
+ * RangeError of output.set() may interrupt the block, and the call runs the host encoder
+ * (lz4mi_host_compress_block), which reproduces that store by store.
  * Returns the number of bytes the reference would report written (>= 0) or a
- * negative status.
+ * negative status (LZ4MI_ERR_RANGE: the reference threw; what it wrote before stays).
  */
 int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
                                    int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off,
@@ -216,6 +219,19 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
 int32_t lz4mi_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len, int32_t block_size,
                              int32_t* table, uint8_t* out, const uint64_t* out_off, uint32_t* comp_len, uint32_t flags,
                              void* stream);
+
+/*
+ * Host-CPU block encoder (the routing of SURVEY.md §8b: serial-chain calls run on the calling
+ * thread). Same contract as lz4mi_compress_block_table / lz4mi_compress_chain (host pointers,
+ * no device needed); byte-identical output and table. Used by the JS layer for dependent-block
+ * frames (LZ4.compress's default) and a dictionary's first block, and by
+ * lz4mi_compress_block_table when the output has less room than the worst case.
+ */
+int64_t lz4mi_host_compress_block(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
+                                  int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off);
+int32_t lz4mi_host_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len,
+                                  int32_t block_size, int32_t* table, uint8_t* out, const uint64_t* out_off,
+                                  uint32_t* comp_len);
 
 /*
  * Block index of a device-resident frame, for decoding its blocks on several devices

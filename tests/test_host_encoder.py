@@ -1,0 +1,104 @@
+"""The host-CPU block encoder of the drop-in's routing (lz4mi_host_compress_block /
+lz4mi_host_compress_chain, csrc/lz4mi_host.cpp; SURVEY.md §8b "Routing"): product code
+written fresh, checked here on CPU against the reference-generated golden vectors —
+the same fixtures that pin the oracle — with no GPU and no oracle in the path under test
+(the oracle only regenerates seeded inputs)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import cases_of, golden_bytes
+
+lz4mi = pytest.importorskip("lz4mi")
+
+
+def _src_of(case):
+    if "gen" in case:
+        g = case["gen"]
+        return O.generate(g["gen"], g["seed"], g["n"])
+    return golden_bytes(case["src_file"]).copy()
+
+
+def _host_block(src):
+    out = np.zeros(lz4mi.compress_bound(src.size), dtype=np.uint8)
+    t = np.zeros(16384, dtype=np.int32)
+    n = lz4mi.host_compress_raw(src, out, 0, src.size, t, 0)
+    return out[:n]
+
+
+def test_host_blocks_match_reference(manifest):
+    for c in cases_of(manifest, "block"):
+        comp = _host_block(_src_of(c))
+        assert comp.size == c["comp_len"], c["name"]
+        assert "%08x" % lz4mi.xxh32(comp) == c["comp_xxh"], c["name"]
+        if c["comp_file"]:
+            assert np.array_equal(comp, golden_bytes(c["comp_file"])), c["name"]
+
+
+def test_host_chain_with_carried_table(manifest):
+    """blockCompress.js with one table carried over three calls into one output buffer."""
+    (c,) = cases_of(manifest, "block_chain")
+    g = c["gen"]
+    src = O.generate(g["gen"], g["seed"], g["n"])
+    out = np.zeros(400000, dtype=np.uint8)
+    table = np.full(16384, c["table_init"], dtype=np.int32)
+    pos = c["out_off0"]
+    for i, (start, n, expect) in enumerate(c["segments"]):
+        w = lz4mi.host_compress_raw(src, out, start, n, table, pos)
+        assert w == expect
+        pos += w
+        if i == 0:
+            assert np.array_equal(table.view(np.uint8), golden_bytes(c["table1_file"]))
+    assert np.array_equal(out[:pos], golden_bytes(c["out_file"]))
+    assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_final_file"]))
+
+
+def test_host_raw_edges_rangeerror_and_drops(manifest):
+    """Output too small: the reference's RangeError of output.set (bytes and table entries
+    written before it kept) and byte stores past the end dropped; F7 (five arguments) = 0."""
+    (g,) = cases_of(manifest, "compress_raw_edges")
+    for c in g["cases"]:
+        src = golden_bytes(c["src_file"]).copy()
+        out = np.zeros(c["out_len"], dtype=np.uint8)
+        table = np.zeros(16384, dtype=np.int32)
+        try:
+            v = lz4mi.host_compress_raw(src, out, c["start"], c["len"], table, None if c["five_args"] else c["out_off"])
+            assert c["ok"] and v == c["value"], c["name"]
+        except lz4mi.Lz4miError as e:
+            assert not c["ok"] and e.status == lz4mi.ERR_RANGE and c["error_name"] == "RangeError", c["name"]
+        assert np.array_equal(out, golden_bytes(c["out_file"])), c["name"]
+        assert np.array_equal(table.view(np.uint8), golden_bytes(c["table_file"])), c["name"]
+
+
+def test_host_dependent_frames_match_reference(manifest):
+    """LZ4.compress's default (dependent blocks, one table carried across the frame) through
+    the host chain: every dependent golden frame without a dictionary, byte for byte."""
+    (g,) = cases_of(manifest, "frames")
+    inputs = {"text": ("text", 5, 300000), "copy": ("copy", 6, 150000), "tiles216": ("tiles216", 8, 1 << 20),
+              "random": ("random", 9, 70000)}
+    from lz4mi import frame as F, shard
+    done = 0
+    for f in g["frames"]:
+        if f["indep"] or "dict" in f or "dict_text" in f or f["input"] not in inputs:
+            continue
+        data = O.generate(*inputs[f["input"]])[: f["n"]]
+        table = np.zeros(16384, dtype=np.int32)
+        blocks = lz4mi.compress_chain(data, 0, data.size, f["block"], table, host=True)
+        raws = [data[p:p + f["block"]] for p in range(0, data.size, f["block"])]
+        body = shard.block_records(raws, blocks)
+        add = f.get("add_size", True)
+        hdr = F.header(f["block"], False, f["checksum"], data.size if add else None)
+        frame = np.concatenate([np.frombuffer(hdr, dtype=np.uint8), body, np.zeros(4, dtype=np.uint8)] +
+                               ([np.array([lz4mi.xxh32(data)], dtype="<u4").view(np.uint8)] if f["checksum"] else []))
+        assert frame.size == f["frame_len"], f
+        assert "%08x" % lz4mi.xxh32(frame) == f["frame_xxh"], f
+        done += 1
+    assert done >= 8
+
+
+@pytest.mark.parametrize("kind", ["random", "repetitive", "tiles216"])
+def test_host_digest_manifest_4mib(manifest, kind):
+    (g,) = cases_of(manifest, "digest_4mib")
+    for r in [r for r in g["rows"] if r["gen"] == kind][:4]:
+        comp = _host_block(O.generate(kind, r["seed"], r["n"]))
+        assert comp.size == r["comp_len"] and "%08x" % lz4mi.xxh32(comp) == r["comp_xxh"], r
