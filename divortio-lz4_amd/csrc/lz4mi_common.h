@@ -16,6 +16,7 @@ __device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
 }
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+constexpr int kWaveShr1 = 0x138;   // lane l gets lane l - 1 (GFX9 wave_shr:1; lane 0 gets `old`)
 
 // Wave-wide inclusive prefix sum (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {

@@ -85,7 +85,7 @@ constexpr int kChunk = 1024;                  // compressed bytes parsed per ste
 constexpr int kPad = 64;                      // lookahead for sequences straddling the chunk end
 constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular sequence may touch
 constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
-constexpr int kMaxSeq = kChunk / 3 + 4;       // every non-final sequence is >= 3 bytes
+constexpr int kMaxSeq = kChunk / 3 + 3;       // tokens starting in the chunk: every non-final sequence is >= 3 bytes
 constexpr uint32_t kWarm = 512;               // speculative walks start this far before their segment
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
@@ -98,26 +98,24 @@ constexpr int kPeriodBulk = 1024;             // longer periodic runs are genera
 constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
 
 struct DecShared {
-    uint32_t stage[kStageWords];
     union {
+        uint4 t_seq[kMaxSeq];     // per sequence: {output start (block-relative), literal source (chunk-
+                                  //  relative) | literal length << 16, match offset | match length << 16
+                                  //  (0: final literal-only sequence), source remapped by remap_src}
         struct {
-            uint32_t t_out[kMaxSeq];      // output start of each sequence (block-relative)
-            int32_t t_rsrc[kMaxSeq];      // round 1: a match's source mapped back to finished output (remap_src)
+            uint16_t nxt2[kChunk];   // parse: token 2 steps after p
+            uint16_t nxt4[kChunk];   // parse: token 4 steps after p (warm-up walks)
         };
-        uint16_t nxt4[kChunk];            // parse: token 4 steps after p (warm-up walks)
-    };
-    union {
-        uint2 t_info[kMaxSeq];            // {literal source (chunk-relative) | literal length << 16,
-                                          //  match offset | match length << 16 (0: final literal-only sequence)}
-        uint16_t nxt2[kChunk];            // parse: token 2 steps after p
     };
     union {
         uint16_t nxt[kLim];       // parse: next-token table
         uint32_t pme[kLim / 2];   // output: ends of the pending matches
     };
     uint32_t pms[kMaxSeq];        // output: starts of the pending matches
+    uint32_t stage[kStageWords];
 };
 static_assert(kLim / 2 >= kMaxSeq, "pending list must fit in the next-token table");
+static_assert(offsetof(DecShared, stage) % 16 == 0 && offsetof(DecShared, pme) % 16 == 0, "16-byte aligned rows");
 
 // LDS a whole-wave periodic run may copy its pattern into, by phase of the
 // chunk: round 1 (the pending list is not built yet), rounds 2+ (the staged
@@ -130,12 +128,13 @@ struct PatBuf {
 __device__ __forceinline__ PatBuf no_pat() { return PatBuf{nullptr, 0}; }   // literal runs
 __device__ __forceinline__ PatBuf pat_round1(DecShared& S) { return PatBuf{S.pms, (int32_t)sizeof(S.pms)}; }
 __device__ __forceinline__ PatBuf pat_rounds(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(S.stage)}; }
-__device__ __forceinline__ PatBuf pat_all(DecShared& S) { return PatBuf{S.stage, (int32_t)sizeof(DecShared)}; }
+__device__ __forceinline__ PatBuf pat_all(DecShared& S) { return PatBuf{(uint32_t*)&S, (int32_t)sizeof(DecShared)}; }
 __device__ __forceinline__ PatBuf pat_cut(DecShared& S) {
     return PatBuf{S.pme, (int32_t)(sizeof(DecShared) - offsetof(DecShared, pme))};
 }
-static_assert(offsetof(DecShared, pms) == offsetof(DecShared, pme) + sizeof(uint32_t) * (kLim / 2),
-              "the cut pattern buffer spans pme and pms");
+static_assert(offsetof(DecShared, pms) == offsetof(DecShared, pme) + sizeof(uint32_t) * (kLim / 2) &&
+              offsetof(DecShared, stage) == offsetof(DecShared, pms) + sizeof(uint32_t) * kMaxSeq,
+              "the cut pattern buffer spans pme, pms and the stage");
 
 struct Ctx {
     const uint8_t* blk;   // compressed block
@@ -186,7 +185,7 @@ __device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
 // ---------------------------------------------------------------- parsing
 // Position of the token after the one at p (chunk-relative), or kEnd / kStop.
 // Exact for any field lengths.
-__device__ uint32_t next_token(const uint8_t* s, uint32_t p, uint32_t rem) {
+__device__ __forceinline__ uint32_t next_token(const uint8_t* s, uint32_t p, uint32_t rem) {
     if (p >= (uint32_t)kLim) return kStop;
     uint32_t tok = s[p];
     uint32_t q = p + 1;
@@ -230,6 +229,73 @@ __device__ __forceinline__ uint32_t next_fast(const uint8_t* s, uint32_t p, uint
     return v;
 }
 
+// The fast next-token table: positions 4w .. 4w+3 (w = lane + 64 r) from the stage
+// dwords w and w+1, next = p + 1 + [literal ext] + literals + 2 + [match ext], i.e. every
+// length field taken to be at most one extension byte. Valid while no field or next()
+// can reach the block's end (rem > kFastRem). A literal field of 2+ bytes (ext byte 255)
+// stops the chain there (0xFFFF); a match field of 2+ bytes is caught on the true tokens
+// (table build) and the chunk re-parsed with the exact table. Values past the window stay
+// raw (<= 1297): every walk ends at them, and a tail past kLim is a cut.
+constexpr uint32_t kFastRem = kLim + 300;
+__device__ __forceinline__ uint32_t next4_half(uint32_t t, uint32_t b1, uint32_t p) {
+    const uint32_t hi = t >> 4;
+    const uint32_t x1 = hi == 15 ? 1u : 0u;
+    const uint32_t ll = x1 ? 15u + b1 : hi;
+    const uint32_t x2 = (t & 15) == 15 ? 1u : 0u;
+    const uint32_t n = p + 3 + x1 + x2 + ll;
+    return (x1 && b1 == 255) ? 0xFFFFu : n;
+}
+// The lane index as a value the compiler cannot hoist out of the chunk loop: per-lane
+// constants derived from it (p + 1, p + 2, ... of every row) would otherwise be computed
+// once and kept in (spilled) registers, their reloads scratch loads that wait, in order,
+// for every store still in flight.
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ void next_table_fast(const uint32_t* stage, uint16_t* nxt, int lane) {
+    static_assert(kChunk % (4 * kWave) == 0, "whole dword rows per lane");
+    lane = opaque(lane);
+    uint32_t d0[kChunk / (4 * kWave)], d1[kChunk / (4 * kWave)];
+#pragma unroll
+    for (int r = 0; r < kChunk / (4 * kWave); ++r) {
+        const uint32_t w = lane + kWave * r;
+        d0[r] = stage[w];
+        d1[r] = stage[w + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < kChunk / (4 * kWave); ++r) {
+        const uint32_t w = lane + kWave * r, p = 4 * w;
+        const uint32_t a = d0[r], b = d1[r];
+        const uint32_t n0 = next4_half(a & 255, (a >> 8) & 255, p);
+        const uint32_t n1 = next4_half((a >> 8) & 255, (a >> 16) & 255, p + 1);
+        const uint32_t n2 = next4_half((a >> 16) & 255, a >> 24, p + 2);
+        const uint32_t n3 = next4_half(a >> 24, b & 255, p + 3);
+        *(uint2*)(nxt + p) = make_uint2(n0 | (n1 << 16), n2 | (n3 << 16));
+    }
+}
+
+// out[p] = in[in[p]] (or in[p] when that is past the chunk): 4 positions per lane, the
+// 16 gathers of a lane issued together.
+__device__ __forceinline__ void jump_table(const uint16_t* in, uint16_t* out, int lane) {
+    constexpr int R = kChunk / (4 * kWave);
+    lane = opaque(lane);
+    uint2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = *(const uint2*)(in + 4 * (lane + kWave * r));
+    uint32_t y[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t a[4] = {v[r].x & 0xFFFFu, v[r].x >> 16, v[r].y & 0xFFFFu, v[r].y >> 16};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[r][j] = a[j] < (uint32_t)kChunk ? in[a[j]] : a[j];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        *(uint2*)(out + 4 * (lane + kWave * r)) = make_uint2(y[r][0] | (y[r][1] << 16), y[r][2] | (y[r][3] << 16));
+}
+
 // Registers loaded by global loads that an explicit wait_vmem() has already
 // covered: redefine them opaquely so the compiler's wait insertion no longer
 // tracks them (it would otherwise wait for every later store before their use).
@@ -247,12 +313,14 @@ __device__ __forceinline__ uint32_t next_of(const uint16_t* nxt, uint32_t p) {
 }
 
 struct SeqInfo {
-    int32_t lit, ll, off, ml;
+    int32_t out, lit, ll, off, ml, rsrc;
 };
-__device__ __forceinline__ SeqInfo seq_info(const DecShared& S, uint32_t k) {
-    uint2 v = S.t_info[k];
-    return SeqInfo{(int32_t)(v.x & 0xFFFF), (int32_t)(v.x >> 16), (int32_t)(v.y & 0xFFFF), (int32_t)(v.y >> 16)};
+__device__ __forceinline__ SeqInfo seq_of(uint4 v) {
+    return SeqInfo{(int32_t)v.x, (int32_t)(v.y & 0xFFFF), (int32_t)(v.y >> 16), (int32_t)(v.z & 0xFFFF),
+                   (int32_t)(v.z >> 16), (int32_t)v.w};
 }
+// one ds_read_b128: everything of sequence k
+__device__ __forceinline__ SeqInfo seq_info(const DecShared& S, uint32_t k) { return seq_of(S.t_seq[k]); }
 
 // History (earlier output of this wave) is read with plain loads: the CU's L1 sees
 // the wave's own completed stores (every read of output follows an s_waitcnt on
@@ -486,17 +554,27 @@ __device__ __forceinline__ bool any_slot(const Slot (&s)[NB]) {
 // hands out this lane's next pieces (sources already complete).
 template <uint32_t KIND, bool TWO, int NB, class Gen>
 __device__ __forceinline__ void pipe(const Ctx& c, DecShared& S, Gen& g) {
+    // (every issued load is consumed by a store before the function returns: a load left
+    // in flight at the exit would make the next write of its registers wait for vmcnt(0),
+    // i.e. for every store in flight)
     Slot s0[NB], s1[NB];
     uint4 a0[NB], b0[NB], a1[NB], b1[NB];
     g.fill(s0);
+    if (!__ballot(any_slot<NB>(s0))) return;
     load_slots<KIND, TWO, NB>(c, S, s0, a0, b0);
     for (;;) {
-        if (!__ballot(any_slot<NB>(s0))) break;
         g.fill(s1);
+        if (!__ballot(any_slot<NB>(s1))) {
+            store_slots<TWO, NB>(c, S, s0, a0, b0);
+            return;
+        }
         load_slots<KIND, TWO, NB>(c, S, s1, a1, b1);
         store_slots<TWO, NB>(c, S, s0, a0, b0);
-        if (!__ballot(any_slot<NB>(s1))) break;
         g.fill(s0);
+        if (!__ballot(any_slot<NB>(s0))) {
+            store_slots<TWO, NB>(c, S, s1, a1, b1);
+            return;
+        }
         load_slots<KIND, TWO, NB>(c, S, s0, a0, b0);
         store_slots<TWO, NB>(c, S, s1, a1, b1);
     }
@@ -529,9 +607,14 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
         if (re <= (int32_t)c.O) return 1;
         if (rs < (int32_t)c.O) return 0;
         uint32_t lo = S.nxt[(uint32_t)(rs - (int32_t)c.O) >> sh];   // last sequence starting at or before rs
-        while (lo + 1 < nseq && (int32_t)S.t_out[lo + 1] <= rs) ++lo;
-        const int32_t t0 = (int32_t)S.t_out[lo];
-        const SeqInfo q = seq_info(S, lo);
+        SeqInfo q = seq_info(S, lo);
+        int32_t nx = lo + 1 < nseq ? (int32_t)S.t_seq[lo + 1].x : INT32_MAX;   // (read together with q)
+        while (nx <= rs) {
+            ++lo;
+            q = seq_info(S, lo);
+            nx = lo + 1 < nseq ? (int32_t)S.t_seq[lo + 1].x : INT32_MAX;
+        }
+        const int32_t t0 = q.out;
         const int32_t ms = t0 + q.ll;
         if (re <= ms) {
             lds = q.lit + (rs - t0);
@@ -555,7 +638,7 @@ struct LSlot {
 struct LaneMatchGen {
     const Ctx& c;
     const DecShared& S;
-    uint32_t bits, rbits;   // rbits: the source was remapped (S.t_rsrc)
+    uint32_t bits, rbits;   // rbits: the source was remapped (SeqInfo::rsrc)
     int lane, q, np;
     int32_t y, n, src;
     // One batch = up to NB pieces of ONE run (runs are >= 16 bytes here, so
@@ -569,10 +652,10 @@ struct LaneMatchGen {
                 const uint32_t bi = __builtin_ctz(bits), k = 64u * bi + lane;
                 bits &= bits - 1;
                 const SeqInfo qi = seq_info(S, k);
-                const int32_t ms = (int32_t)S.t_out[k] + qi.ll;
+                const int32_t ms = qi.out + qi.ll;
                 y = ms;
                 n = (ms + qi.ml > c.cap ? c.cap : ms + qi.ml) - ms;
-                src = (rbits >> bi) & 1u ? S.t_rsrc[k] : ms - qi.off;
+                src = (rbits >> bi) & 1u ? qi.rsrc : ms - qi.off;
                 np = (n + 15) >> 4;
             }
         }
@@ -619,17 +702,25 @@ __device__ __forceinline__ bool any_lslot(const LSlot (&s)[NB]) {
 
 template <int NB, class Gen>
 __device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, Gen& g) {
+    // (as pipe(): no load left in flight at the exit)
     LSlot s0[NB], s1[NB];
     uint4 a0[NB], a1[NB];
     g.template fill<NB>(s0);
+    if (!__ballot(any_lslot<NB>(s0))) return;
     lane_load<NB>(c, s0, a0);
     for (;;) {
-        if (!__ballot(any_lslot<NB>(s0))) break;
         g.template fill<NB>(s1);
+        if (!__ballot(any_lslot<NB>(s1))) {
+            lane_store<NB>(c, S, s0, a0);
+            return;
+        }
         lane_load<NB>(c, s1, a1);
         lane_store<NB>(c, S, s0, a0);
-        if (!__ballot(any_lslot<NB>(s1))) break;
         g.template fill<NB>(s0);
+        if (!__ballot(any_lslot<NB>(s0))) {
+            lane_store<NB>(c, S, s1, a1);
+            return;
+        }
         lane_load<NB>(c, s0, a0);
         lane_store<NB>(c, S, s1, a1);
     }
@@ -684,7 +775,7 @@ struct PieceGen {
     }
 };
 
-// The matches of sequences 64 i + lane for every bit i of `ready` (sources: S.t_rsrc
+// The matches of sequences 64 i + lane for every bit i of `ready` (sources: SeqInfo::rsrc
 // where `rbits` says so), two sequence rows per batch.
 __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t ready, uint32_t rbits, int lane,
                                            uint32_t nseq) {
@@ -703,10 +794,10 @@ __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t 
             if (rd) {
                 const uint32_t k = 64u * i + (uint32_t)lane;
                 const SeqInfo q = seq_info(S, k);
-                const int32_t ms = (int32_t)S.t_out[k] + q.ll;
+                const int32_t ms = q.out + q.ll;
                 y = ms;
                 n = (ms + q.ml > c.cap ? c.cap : ms + q.ml) - ms;
-                src = (rbits >> i) & 1u ? S.t_rsrc[k] : ms - q.off;
+                src = (rbits >> i) & 1u ? q.rsrc : ms - q.off;
             }
             const uint32_t np = rd ? (uint32_t)(n + 15) >> 4 : 0u;
             const uint32_t incl = wave_incl_scan(np, lane);
@@ -938,7 +1029,7 @@ __device__ __forceinline__ uint32_t f1_changes(const Ctx& c, int32_t ms, int32_t
 // (periodic copy: its source bytes before its start are final when it runs), and every
 // rewrite is applied (blockDecompress.js:219-250: out[p] = out[p - off] for
 // p in [ms + ml - 8, ms), after the copy). Later chunks then read the fixed output.
-__device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t nseq, bool cut, int64_t cut_ms,
+__device__ void f1_fixup(const Ctx c, const DecShared& S, int lane, uint32_t nseq, bool cut, int64_t cut_ms,
                          int32_t coff, int32_t cml) {
     int64_t lo = INT64_MAX;
     const uint32_t n = nseq + (cut ? 1u : 0u);
@@ -947,7 +1038,7 @@ __device__ void f1_fixup(const Ctx& c, const DecShared& S, int lane, uint32_t ns
         int32_t off, ml;
         if (k < nseq) {
             const SeqInfo q = seq_info(S, k);
-            ms = (int64_t)S.t_out[k] + q.ll;
+            ms = (int64_t)q.out + q.ll;
             off = q.off;
             ml = q.ml;
         } else {
@@ -1015,21 +1106,27 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         PROF_COUNT(10, 1);
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
         // the previous chunk's output phase, ahead of its stores) -------------
+        // (each branch writes the stage itself: a write after the join would wait for the
+        // fresh loads of the first branch on both, i.e. for every store still in flight)
         if (!have_pf || pf_at != c.ip) {
-            pf0 = stage_piece(c, (int64_t)c.ip + 16 * lane);
-            if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, (int64_t)c.ip + 16 * (kWave + lane));
-            settle(pf0);
-            settle(pf1);
+            const uint4 a = stage_piece(c, (int64_t)c.ip + 16 * opaque(lane));
+            uint4 b = make_uint4(0, 0, 0, 0);
+            if (lane < kStageWords / 4 - kWave) b = stage_piece(c, (int64_t)c.ip + 16 * (kWave + opaque(lane)));
+            __builtin_memcpy((uint8_t*)S.stage + 16 * lane, &a, 16);
+            if (lane < kStageWords / 4 - kWave) __builtin_memcpy((uint8_t*)S.stage + 16 * (kWave + lane), &b, 16);
+        } else {
+            __builtin_memcpy((uint8_t*)S.stage + 16 * lane, &pf0, 16);
+            if (lane < kStageWords / 4 - kWave) __builtin_memcpy((uint8_t*)S.stage + 16 * (kWave + lane), &pf1, 16);
         }
         have_pf = false;
-        __builtin_memcpy((uint8_t*)S.stage + 16 * lane, &pf0, 16);
-        if (lane < kStageWords / 4 - kWave) __builtin_memcpy((uint8_t*)S.stage + 16 * (kWave + lane), &pf1, 16);
         __syncthreads();
         const uint8_t* s = (const uint8_t*)S.stage;
         const uint32_t rem = (uint32_t)(c.in_len - c.ip);
 
         const uint32_t seg0 = 16u * lane, seg1 = seg0 + 16;
         uint32_t vis, tail;
+        bool fast_tab = rem > kFastRem;
+    parse:
         {
         PROF(0);
         // Wave priorities by phase (the 4 waves of a SIMD are in different phases):
@@ -1038,12 +1135,19 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         // mix -2.5 %, copy -1.5 % (A/B in one process, profiles/r02j/prio_ab.json).
         __builtin_amdgcn_s_setprio(0);
         // ---- 2. next-token table -----------------------------------------
+        // Away from the block's end (fast_tab) four positions per lane from two stage
+        // dwords, assuming length fields of at most one extension byte: a token whose
+        // literal field runs on (b1 == 255) stops the chain (the cut path parses it), and
+        // a match field that runs on (checked on the true tokens in the table build) sends
+        // the chunk back here for the exact table. Near the end: the exact table.
         uint16_t* nxt = S.nxt;
-        {   // all positions' fields read at once; the rare longer length fields afterwards
-            static_assert(kLim % kWave == 0 && kChunk % kWave == 0, "whole rows per lane");
+        if (fast_tab) {
+            next_table_fast(S.stage, nxt, lane);
+        } else {   // all positions' fields read at once; the rare longer length fields afterwards
+            static_assert(kChunk % kWave == 0, "whole rows per lane");
             uint32_t slm = 0;
 #pragma unroll
-            for (int i = 0; i < kLim / kWave; ++i) {
+            for (int i = 0; i < kChunk / kWave; ++i) {
                 bool slow;
                 const uint32_t v = next_fast(s, lane + kWave * i, rem, slow);
                 slm |= (slow ? 1u : 0u) << i;
@@ -1058,17 +1162,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         }
         __syncthreads();
         // 2- and 4-step jumps (the warm-up walks only need where the chain lands)
-#pragma unroll
-        for (int i = 0; i < kChunk / kWave; ++i) {
-            const uint32_t a = nxt[lane + kWave * i];
-            S.nxt2[lane + kWave * i] = a < (uint32_t)kChunk ? nxt[a] : (uint16_t)a;
-        }
+        jump_table(nxt, S.nxt2, lane);
         __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kChunk / kWave; ++i) {
-            const uint32_t a = S.nxt2[lane + kWave * i];
-            S.nxt4[lane + kWave * i] = a < (uint32_t)kChunk ? S.nxt2[a] : (uint16_t)a;
-        }
+        jump_table(S.nxt2, S.nxt4, lane);
         __syncthreads();
 #if LZ4MI_ABLATE == 3
         c.ip += kChunk;
@@ -1095,7 +1191,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         uint32_t es = vis ? seg0 + __builtin_ctz(vis) : x;
         uint32_t nE = 0;
         for (int it = 0; it <= kWave; ++it) {
-            uint32_t pes = __shfl_up(es, 1, kWave), px = __shfl_up(x, 1, kWave);
+            // lane l - 1's values by DPP wave_shr:1 (a VALU operand, not an LDS permute)
+            const uint32_t pes = dpp<kWaveShr1>(0u, es), px = dpp<kWaveShr1>(0u, x);
             nE = lane == 0 ? 0u : (pes >= seg0 ? pes : px);
             bool valid = nE >= seg1 ? (vis == 0 && x == nE) : ((vis >> (nE - seg0)) & 1u) != 0;
             uint64_t bad = __ballot(!valid);
@@ -1116,6 +1213,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (nE >= seg1) vis = 0;
         else vis &= ~((1u << (nE - seg0)) - 1u);
         tail = lane_of(x, kWave - 1);   // where the chain leaves the chunk
+        if (tail > (uint32_t)kLim && tail < kEnd) tail = kStop;   // (fast table: raw positions past the window)
         }
         (void)seg1;
         const uint64_t has = __ballot(vis != 0);
@@ -1125,8 +1223,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (!cut && tail < kEnd && (int64_t)c.ip + tail < c.in_len) {
             // the next chunk's bytes: loaded while this chunk's table is built
             int64_t nip = (int64_t)c.ip + tail;
-            pf0 = stage_piece(c, nip + 16 * lane);
-            if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+            pf0 = stage_piece(c, nip + 16 * opaque(lane));
+            if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + opaque(lane)));
             pf_at = nip;
             have_pf = true;
         }
@@ -1138,51 +1236,95 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
         PROF(2);
         // ---- 4. sequence table -----------------------------------------
+        // A lane's tokens (those of its segment, in order) four at a time, each group's
+        // byte reads issued together (two LDS round trips per group, not per token);
+        // output starts by wave prefix sums; errors in the reference's order.
         const uint32_t cnt = __popc(vis) - ((cut && lane == last_lane) ? 1u : 0u);
         const uint32_t incl = wave_incl_scan(cnt, lane);
         const uint32_t base = incl - cnt;
         const uint32_t nseq = lane_of(incl, kWave - 1);
         uint32_t run = 0;
+        bool rerun = false;   // a true token's match length runs on past one byte (fast table)
         {
-            uint32_t m = vis, k = base;
-            for (uint32_t i = 0; i < cnt; ++i) {
-                const uint32_t p = seg0 + __builtin_ctz(m);
-                m &= m - 1;
-                const uint32_t tok = s[p], b1 = s[p + 1];
-                uint32_t q = p + 1, ll = tok >> 4;
-                if (ll == 15) {
-                    if (b1 != 255) { ll += b1; ++q; }
-                    else { uint32_t bb; do { bb = s[q++]; ll += bb; } while (bb == 255); }
+            uint32_t m = vis;
+            for (uint32_t g = 0; __ballot(g < cnt) != 0; g += 4) {
+                uint32_t p[4], tok[4], b1[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    p[j] = g + j < cnt ? seg0 + __builtin_ctz(m) : seg0;
+                    if (g + j < cnt) m &= m - 1;
+                    tok[j] = s[p[j]];
+                    b1[j] = s[p[j] + 1];
                 }
-                const uint32_t lit = q;
-                q += ll;
-                uint32_t off = 0, ml = 0;
-                if (q < rem) {
-                    off = (uint32_t)s[q] | ((uint32_t)s[q + 1] << 8);
-                    ml = tok & 15;
-                    if (ml == 15) {
-                        uint32_t bb = s[q + 2];
-                        if (bb != 255) ml += bb;
-                        else { uint32_t r = q + 2; do { bb = s[r++]; ml += bb; } while (bb == 255); }
+                uint32_t q[4], lit[4], ll[4], o0[4], o1[4], mb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t x1 = (tok[j] >> 4) == 15 ? 1u : 0u;
+                    ll[j] = x1 ? 15u + b1[j] : tok[j] >> 4;
+                    lit[j] = p[j] + 1 + x1;
+                    q[j] = lit[j] + ll[j];
+                    const uint32_t qa = q[j] + 2 < (uint32_t)kLim ? q[j] : 0u;   // (a long literal run: slow below)
+                    o0[j] = s[qa];
+                    o1[j] = s[qa + 1];
+                    mb[j] = s[qa + 2];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (g + j >= cnt) continue;
+                    uint32_t llj = ll[j], litj = lit[j], qj = q[j], off = 0, ml = 0;
+                    if ((tok[j] >> 4) == 15 && b1[j] == 255) {   // literal length field of 2+ bytes
+                        uint32_t r = p[j] + 1, bb;
+                        llj = 15;
+                        do { bb = s[r++]; llj += bb; } while (bb == 255);
+                        litj = r;
+                        qj = r + llj;
+                        if (qj < rem) { o0[j] = s[qj]; o1[j] = s[qj + 1]; mb[j] = s[qj + 2]; }
                     }
-                    ml += 4;
+                    if (qj < rem) {
+                        off = o0[j] | (o1[j] << 8);
+                        ml = tok[j] & 15;
+                        if (ml == 15) {
+                            if (mb[j] != 255) {
+                                ml += mb[j];
+                            } else {
+                                rerun |= fast_tab;
+                                uint32_t r = qj + 2, bb;
+                                do { bb = s[r++]; ml += bb; } while (bb == 255 && r < (uint32_t)kLim);
+                            }
+                        }
+                        ml += 4;
+                    }
+                    const uint32_t k = base + g + j;
+                    S.t_seq[k] = make_uint4(run, litj | (llj << 16), off | (ml << 16), 0u);
+                    run += llj + ml;
                 }
-                S.t_info[k] = make_uint2(lit | (ll << 16), off | (ml << 16));
-                S.t_out[k] = run;
-                run += ll + ml;
-                ++k;
             }
+        }
+        if (__ballot(rerun)) {   // the fast table assumed a one-byte match length field
+            fast_tab = false;
+            wait_vmem();          // (no load in flight into the parse: its registers are free)
+            settle(pf0);
+            settle(pf1);
+            __syncthreads();
+            goto parse;
         }
         const uint32_t lincl = wave_incl_scan(run, lane);
         const uint32_t lbase = lincl - run;
         const int64_t total = lane_of(lincl, kWave - 1);
         uint32_t first_err = 0xFFFFFFFFu;
-        for (uint32_t k = base; k < base + cnt; ++k) {
-            const int64_t os = c.O + lbase + S.t_out[k];
-            S.t_out[k] = (uint32_t)os;
-            const SeqInfo q = seq_info(S, k);
-            const uint32_t e = seq_error(c, os, (int64_t)c.ip + q.lit, q.ll, q.off, q.ml);
-            if (e && first_err == 0xFFFFFFFFu) first_err = (k << 3) | e;
+        for (uint32_t g = 0; __ballot(g < cnt) != 0; g += 4) {
+            SeqInfo q[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] = seq_info(S, base + (g + j < cnt ? g + j : 0u));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (g + j >= cnt) continue;
+                const uint32_t k = base + g + j;
+                const int64_t os = c.O + lbase + (uint32_t)q[j].out;
+                S.t_seq[k].x = (uint32_t)os;
+                const uint32_t e = seq_error(c, os, (int64_t)c.ip + q[j].lit, q[j].ll, q[j].off, q[j].ml);
+                if (e && first_err == 0xFFFFFFFFu) first_err = (k << 3) | e;
+            }
         }
         first_err = wave_min(first_err);
         __syncthreads();
@@ -1242,8 +1384,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (cut) {   // the next chunk's bytes: their loads go out before this chunk's stores
             int64_t nip = cq < c.in_len ? cq : c.in_len;
             if (nip < c.in_len) {
-                    pf0 = stage_piece(c, nip + 16 * lane);
-                if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + lane));
+                    pf0 = stage_piece(c, nip + 16 * opaque(lane));
+                if (lane < kStageWords / 4 - kWave) pf1 = stage_piece(c, nip + 16 * (kWave + opaque(lane)));
                     pf_at = nip;
                 have_pf = true;
             }
@@ -1262,20 +1404,20 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         uint32_t msh = 4;
         while ((total >> msh) >= kLim) ++msh;
         for (uint32_t k = lane; k < nseq; k += kWave) {
-            const uint32_t t0 = S.t_out[k] - (uint32_t)c.O;
-            const uint32_t t1 = (k + 1 < nseq ? S.t_out[k + 1] : (uint32_t)(c.O + total)) - (uint32_t)c.O;
+            const uint32_t t0 = S.t_seq[k].x - (uint32_t)c.O;
+            const uint32_t t1 = (k + 1 < nseq ? S.t_seq[k + 1].x : (uint32_t)(c.O + total)) - (uint32_t)c.O;
             for (uint32_t b = (t0 + (1u << msh) - 1) >> msh; (b << msh) < t1; ++b) S.nxt[b] = (uint16_t)k;
         }
         __syncthreads();
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         uint32_t ready = 0;   // bit i: ... is written by this lane in this round
-        uint32_t rbits = 0;   // bit i: ... reads a remapped source (S.t_rsrc)
+        uint32_t rbits = 0;   // bit i: ... reads a remapped source (SeqInfo::rsrc)
         for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
             const uint32_t k = 64 * i + lane;
             Run L = no_run(), M = no_run(), ML = no_run();
             if (k < nseq) {
-                const int32_t t0 = (int32_t)S.t_out[k];
                 const SeqInfo q = seq_info(S, k);
+                const int32_t t0 = q.out;
                 if (q.ll) L = Run{t0, q.ll, q.lit, 0, R_LDS};
                 M = match_run(c, t0 + q.ll, q.off, q.ml);
                 if (M.n == 0) {
@@ -1288,7 +1430,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     if (r == 1) {
                         M.src = rs;
                         if (c.out_off + rs < 16) M.kind = R_BYTES;
-                        S.t_rsrc[k] = rs;
+                        S.t_seq[k].w = (uint32_t)rs;
                         rbits |= 1u << i;
                     } else if (r == 2) {
                         ML = Run{M.y, M.n, li, 0, R_LDS};
@@ -1332,7 +1474,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     const uint32_t idx = np + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
                     const SeqInfo q = seq_info(S, k);
-                    const int32_t ms = (int32_t)S.t_out[k] + q.ll;
+                    const int32_t ms = q.out + q.ll;
                     S.pms[idx] = (uint32_t)ms;
                     S.pme[idx] = (uint32_t)(ms + q.ml > c.cap ? c.cap : ms + q.ml);
                 }
@@ -1350,7 +1492,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 if ((pend >> i) & 1u) {
                     const uint32_t k = 64 * i + lane;
                     const SeqInfo q = seq_info(S, k);
-                    M = match_run(c, (int32_t)S.t_out[k] + q.ll, q.off, q.ml);
+                    M = match_run(c, q.out + q.ll, q.off, q.ml);
                     // first pending match ending past the source start: ready if it starts at or past the source end
                     const int32_t rs = M.src, re = match_src_end(M);
                     uint32_t lo = 0, hi = np;
@@ -1397,7 +1539,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             uint32_t dv = 0;
             for (uint32_t k = lane; k < nseq; k += kWave) {
                 const SeqInfo q = seq_info(S, k);
-                dv |= f1_changes(c, (int32_t)S.t_out[k] + q.ll, q.off, q.ml);
+                dv |= f1_changes(c, q.out + q.ll, q.off, q.ml);
             }
             if (__ballot(dv & 2u)) { status = -9; break; }
             if (__ballot(dv)) f1_fixup(c, S, lane, nseq, false, 0, 0, 0);
