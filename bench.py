@@ -387,6 +387,37 @@ def reference_benchmark(with_js):
     return out
 
 
+def single_block(torch, lz4mi, batch, reps=5):
+    """One 4 MiB block through the raw-block C-ABI with host buffers (LZ4.compressRaw /
+    LZ4.decompressRaw: lz4mi_compress_block_table — the chain kernel with the caller's table
+    in LDS — and lz4mi_decompress_blocks with nblocks = 1), PCIe included, median of `reps`
+    calls; the host encoder (lz4mi_host_compress_block, the layer's route for serial-chain
+    calls) beside it. Latency, not throughput: one block is one wave."""
+    import numpy as np
+    src = batch.raw[:BLOCK].cpu().numpy()
+    out = np.zeros(lz4mi.compress_bound(BLOCK), dtype=np.uint8)
+    res = {}
+    for name, fn in (("compressRaw_gpu", lz4mi.compress_raw), ("compressRaw_host", lz4mi.host_compress_raw)):
+        ts = []
+        for _ in range(reps):
+            t = np.zeros(16384, dtype=np.int32)
+            t0 = time.perf_counter()
+            n = fn(src, out, 0, BLOCK, t, 0)
+            ts.append(time.perf_counter() - t0)
+        res[name + "_ms"] = round(sorted(ts)[len(ts) // 2] * 1e3, 3)
+    comp = out[:n].copy()
+    dec = np.zeros(BLOCK, dtype=np.uint8)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        w = lz4mi.decompress_raw(comp, 0, comp.size, dec, 0)
+        ts.append(time.perf_counter() - t0)
+    res["decompressRaw_gpu_ms"] = round(sorted(ts)[len(ts) // 2] * 1e3, 3)
+    res["verified"] = bool(w == BLOCK and np.array_equal(dec, src))
+    res["workload"] = "one 4 MiB block of the bench's tiles216 batch, host buffers, fresh table, median of %d calls" % reps
+    return res
+
+
 def pmc_traffic(lz4mi, n, gen, name="pmc_traffic.json"):
     """HBM bytes per launch (decode: pmc_traffic.json, compress: pmc_traffic_compress.json)
     from the committed rocprofv3 PMC passes, used only when they were measured on this exact
@@ -446,6 +477,7 @@ def main():
     ms_per_step = d_wall / args.steps * 1e3
 
     napi = napi_e2e(batch) if args.napi and rank == 0 and world == 1 else None
+    single = single_block(torch, lz4mi, batch) if args.napi and rank == 0 and world == 1 else None
     c_base = c_cpu_baseline(batch, cpu_threads()) if args.cpu_baseline and rank == 0 and world == 1 else None
 
     extra = {}
@@ -520,6 +552,8 @@ def main():
         line["frame"] = frame
     if extra:
         line["variants"] = extra
+    if single is not None:
+        line["single_block"] = single
     if napi is not None:
         line["napi_end_to_end"] = napi
         line["reference_benchmark"] = reference_benchmark(bool(args.cpu_baseline))

@@ -60,6 +60,9 @@ __device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l) {
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return (uint64_t)uniform((uint32_t)v) | ((uint64_t)uniform((uint32_t)(v >> 32)) << 32);
+}
 
 // Bytes [sh, sh+4) of the little-endian pair (lo, hi), sh in 0..3.
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh) {

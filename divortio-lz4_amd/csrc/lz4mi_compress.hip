@@ -64,6 +64,43 @@ __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
 }
 
+#ifndef LZ4MI_SHFL_READLANE
+#define LZ4MI_SHFL_READLANE 1   // 0: the two per-batch lane gathers as LDS permutes (A/B switch)
+#endif
+
+// Lanes 8g .. 8g+7 get v of lane g (g < 8): eight v_readlane, no LDS permute round trip.
+__device__ __forceinline__ int32_t group_val(int32_t v, int g) {
+#if LZ4MI_SHFL_READLANE
+    int32_t r = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t x = (int32_t)__builtin_amdgcn_readlane((uint32_t)v, k);
+        r = g == k ? x : r;
+    }
+    return r;
+#else
+    return __shfl(v, g, kWave);
+#endif
+}
+
+// Lane l gets v of lane 8 (l & 7) + f, f = the first set bit of byte (l & 7) of mm (0 when
+// the byte is 0; `ft` is that lane's own f): per group one scalar bit search + v_readlane.
+__device__ __forceinline__ uint32_t first_val(uint32_t v, uint64_t mm, int lane, int ft) {
+#if LZ4MI_SHFL_READLANE
+    (void)ft;
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t gk = (uint32_t)(mm >> (8 * k)) & 0xFFu;
+        const uint32_t x = __builtin_amdgcn_readlane(v, 8 * k + (gk ? __builtin_ctz(gk) : 0));
+        r = (lane & 7) == k ? x : r;
+    }
+    return r;
+#else
+    return __shfl(v, 8 * (lane & 7) + ft, kWave);
+#endif
+}
+
 // Value of v in lane l, l uniform (a ballot's ctz, a lane count): v_readlane
 // instead of the LDS permute __shfl compiles to (on the chain's critical path).
 __device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -635,7 +672,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             if (cand >= 0 && (p - cand < 1 || p - cand > 65535)) cand = -1;
             // ---- windows: lanes 8k .. 8k+7 hold 128 bytes at probe k and at its candidate
             const int gk = lane >> 3, gt = lane & 7;
-            const int32_t gc = __shfl(cand, gk, kWave);
+            const int32_t gc = group_val(cand, gk);
             uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
             if (gk < K) {
                 xa = ld16(j, (int64_t)i + gk * S + 16 * gt);
@@ -652,7 +689,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             // lane k < K: bytes equal at probe k (m, 128 = the whole window)
             const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
             const int ft = gm ? __builtin_ctz(gm) : 0;
-            const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
+            const uint32_t lmv = first_val(lm, mm, lane, ft);
             const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
             const bool hit = act && cand >= 0 && m >= 4;
             const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;
@@ -946,7 +983,7 @@ __device__ int64_t compress_block_chain2(const CompJob& j, ChainShared& F, int l
             if (cand >= 0 && (cand == p || (uint32_t)(p - cand) > 65535u)) cand = -1;
             if (npend) emit_batch(load_lit());
             const int gk = lane >> 3, gt = lane & 7;
-            const int32_t gc = __shfl(cand, gk, kWave);
+            const int32_t gc = group_val(cand, gk);
             uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
             if (gk < K) {
                 xa = rr16(j, r, (int64_t)i + gk * S + 16 * gt);
@@ -957,7 +994,7 @@ __device__ int64_t compress_block_chain2(const CompJob& j, ChainShared& F, int l
             const uint64_t mm = __ballot(lm < 16);
             const uint32_t gm = (uint32_t)(mm >> (8 * (lane & 7))) & 0xFFu;
             const int ft = gm ? __builtin_ctz(gm) : 0;
-            const uint32_t lmv = __shfl(lm, 8 * (lane & 7) + ft, kWave);
+            const uint32_t lmv = first_val(lm, mm, lane, ft);
             const int32_t m = gm ? 16 * ft + (int32_t)lmv : kSpecW;
             const bool hit = act && cand >= 0 && m >= 4;
             const bool lng = hit && m >= kSpecW && p + kSpecW < matchlimit;

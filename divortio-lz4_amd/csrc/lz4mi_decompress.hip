@@ -56,6 +56,10 @@
 #define LZ4MI_PIECES 1   // ready matches copied piece-parallel (piece_pipe); 0: one lane per match (A/B switch)
 #endif
 
+#ifndef LZ4MI_DEFER
+#define LZ4MI_DEFER 0    // round 1's last piece batch stored during the next chunk's parse (A/B switch)
+#endif
+
 #ifndef LZ4MI_PROFILE
 #define LZ4MI_PROFILE 0  // timing-only variant (tools/): per-phase wall-clock accumulation
 #endif
@@ -599,12 +603,16 @@ struct WaveGen {
 // sequences that wrote it (out[y] = out[y - off] inside a match): 1 = it now
 // lies in output finished by earlier chunks, 2 = in sequence j's literal run
 // (*lds = its stage index), 0 = it straddles sequences / the table start.
+// 3 (with `split`): it starts in sequence j's literal run and goes on into j's match:
+// its first *nlit bytes are literal bytes at stage index *lds, the rest maps on to
+// [rs, re) (finished output) — tiles216's usual reason for a later round (72 % of them).
 // S.nxt doubles as an output -> sequence map during round 1: entry b is the
 // sequence holding output O + (b << sh) (built by the kernel before round 1).
 __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint32_t nseq, uint32_t sh, int32_t& rs,
-                                         int32_t& re, int32_t& lds) {
+                                         int32_t& re, int32_t& lds, int32_t& nlit, bool split) {
+    nlit = 0;
     for (int d = 0; d < 8; ++d) {
-        if (re <= (int32_t)c.O) return 1;
+        if (re <= (int32_t)c.O) return nlit ? 3 : 1;
         if (rs < (int32_t)c.O) return 0;
         uint32_t lo = S.nxt[(uint32_t)(rs - (int32_t)c.O) >> sh];   // last sequence starting at or before rs
         SeqInfo q = seq_info(S, lo);
@@ -617,10 +625,17 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
         const int32_t t0 = q.out;
         const int32_t ms = t0 + q.ll;
         if (re <= ms) {
+            if (nlit) return 0;   // (one split at most)
             lds = q.lit + (rs - t0);
             return 2;
         }
-        if (rs < ms || re > ms + q.ml) return 0;
+        if (rs < ms) {
+            if (!split || nlit || ms - rs > 255 || re > ms + q.ml) return 0;
+            lds = q.lit + (rs - t0);
+            nlit = ms - rs;
+            rs = ms;
+        }
+        if (re > ms + q.ml) return 0;
         rs -= q.off;
         re -= q.off;
     }
@@ -739,6 +754,7 @@ struct PEnt {
     int32_t y, src, n, p0;
 };
 constexpr int kPieceRows = 32;                 // bitmap rows: 2 sequence rows x 64 matches x <= 16 pieces
+constexpr int kPieceBatch = 8;                 // piece rows whose loads are in flight together
 static_assert(2 * kWave * (kLaneBytes / 16) <= kPieceRows * kWave, "bitmap holds two sequence rows");
 static_assert(2 * kWave * sizeof(PEnt) + kPieceRows * 8 <= sizeof(uint32_t) * (kLim / 2 + kMaxSeq),
               "match list and bitmap fit the pending list");
@@ -775,10 +791,29 @@ struct PieceGen {
     }
 };
 
+// Round 1's last piece batch with its loads in flight and its stores not yet issued:
+// they go out during the next chunk's parse (after its walks), so the batch's load round
+// trip overlaps the parse instead of ending the chunk. Only for a chunk that needs nothing
+// after round 1 (no later rounds, no cut sequence, no F1 check: nothing reads its output
+// before the next chunk's output phase, whose opening wait covers these stores).
+struct Deferred {
+    uint4 v[kPieceBatch];
+    int32_t y[kPieceBatch];   // -1: empty slot
+    bool any;
+};
+
+__device__ __forceinline__ void flush_deferred(const Ctx& c, Deferred& d) {
+#pragma unroll
+    for (int j = 0; j < kPieceBatch; ++j)
+        if (d.y[j] >= 0) out16(c.dst + d.y[j], d.v[j]);
+    d.any = false;
+}
+
 // The matches of sequences 64 i + lane for every bit i of `ready` (sources: SeqInfo::rsrc
-// where `rbits` says so), two sequence rows per batch.
+// where `rbits` says so), two sequence rows per batch. With `dfr` the last batch's stores
+// are deferred (Deferred above).
 __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t ready, uint32_t rbits, int lane,
-                                           uint32_t nseq) {
+                                           uint32_t nseq, Deferred& dfr, bool defer, uint32_t nlit_pack) {
     PEnt* L = reinterpret_cast<PEnt*>(S.pme);
     uint64_t* bm = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(S.pme) + 2 * kWave * sizeof(PEnt));
     for (uint32_t i0 = 0; 64u * i0 < nseq; i0 += 2) {
@@ -795,8 +830,9 @@ __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t 
                 const uint32_t k = 64u * i + (uint32_t)lane;
                 const SeqInfo q = seq_info(S, k);
                 const int32_t ms = q.out + q.ll;
-                y = ms;
-                n = (ms + q.ml > c.cap ? c.cap : ms + q.ml) - ms;
+                const int32_t nl = i < 4 ? (int32_t)((nlit_pack >> (8 * i)) & 255u) : 0;   // split prefix
+                y = ms + nl;
+                n = (ms + q.ml > c.cap ? c.cap : ms + q.ml) - y;
                 src = (rbits >> i) & 1u ? q.rsrc : ms - q.off;
             }
             const uint32_t np = rd ? (uint32_t)(n + 15) >> 4 : 0u;
@@ -813,7 +849,29 @@ __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t 
         }
         __syncthreads();
         PieceGen g{L, bm, P, 0u, -1, lane};
-        lane_pipe<kB>(c, S, g);
+        // kPieceBatch rows at a time, all loads before all stores: every slot loads (an empty
+        // one the block's first 16 bytes), so the loads are straight-line code and each store
+        // waits only for its own load (counted vmcnt), not for every store in flight
+        while (64u * g.t < P) {
+            LSlot sl[kPieceBatch];
+            uint4 v[kPieceBatch];
+            g.template fill<kPieceBatch>(sl);
+#pragma unroll
+            for (int j = 0; j < kPieceBatch; ++j) {
+                const u32x4_t t = *(const u32x4_t*)(c.dst + (sl[j].w ? sl[j].a : 0));
+                v[j] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+            if (defer && 64u * g.t >= P && 64u * (i0 + 2) >= nseq) {   // the chunk's last batch
+#pragma unroll
+                for (int j = 0; j < kPieceBatch; ++j) {
+                    dfr.v[j] = v[j];
+                    dfr.y[j] = sl[j].w ? sl[j].y : -1;
+                }
+                dfr.any = true;
+                break;
+            }
+            lane_store<kPieceBatch>(c, S, sl, v);
+        }
         __syncthreads();   // the next batch rewrites the list
     }
 }
@@ -947,14 +1005,18 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         if (q < np) out16(c.dst + L.y + d0, v0);
         if (q + 1 < np) out16(c.dst + L.y + d1, v1);
     }
-    if (__ballot(n > 0 && n < 16)) {                       // shorter runs: two overlapping 8/4/2/1-byte stores
-        if (n > 0 && n < 16) {
-            const uint32_t w = n >= 8 ? 8u : n >= 4 ? 4u : n >= 2 ? 2u : 1u;
-            const uint4 v0 = stage16(S.stage, L.src);
-            const uint4 v1 = stage16(S.stage, L.src + n - (int32_t)w);
+    if (__ballot(n > 0 && n < 16)) {                       // shorter runs: 8/4/2/1-byte pieces by the bits of n
+        if (n > 0 && n < 16) {                             // (one stage read, no per-width branches)
+            const uint4 v = stage16(S.stage, L.src);
+            uint8_t* d = c.dst + L.y;
+            uint64_t lo = v.x | ((uint64_t)v.y << 32);
+            const uint64_t hi = v.z | ((uint64_t)v.w << 32);
+            int32_t o = 0;
             if (LZ4MI_ABLATE != 4) {
-                store_w(c.dst + L.y, v0, w);
-                store_w(c.dst + L.y + n - (int32_t)w, v1, w);
+                if (n & 8) { __builtin_memcpy(d, &lo, 8); lo = hi; o = 8; }
+                if (n & 4) { const uint32_t t = (uint32_t)lo; __builtin_memcpy(d + o, &t, 4); lo >>= 32; o += 4; }
+                if (n & 2) { const uint16_t t = (uint16_t)lo; __builtin_memcpy(d + o, &t, 2); lo >>= 16; o += 2; }
+                if (n & 1) d[o] = (uint8_t)lo;
             }
         }
     }
@@ -1082,12 +1144,16 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
 
+    // the block's scalars in SGPRs (readfirstlane): as VGPRs the compiler would keep
+    // per-lane copies of values derived from them and spill those to scratch
+    const uint64_t in_off = uniform64(a.in_off[b]), out_off = uniform64(a.out_off[b]);
+    const uint32_t out_cap = uniform(a.out_cap[b]);
     Ctx c;
-    c.blk = a.in + a.in_off[b];
-    c.in_len = (int32_t)a.in_len[b];
-    c.out_off = (int64_t)a.out_off[b];
-    c.dst = a.out + a.out_off[b];
-    c.cap = a.out_cap[b] > 0x7FFFFFFFu ? 0x7FFFFFFF : (int32_t)a.out_cap[b];
+    c.blk = a.in + in_off;
+    c.in_len = (int32_t)uniform(a.in_len[b]);
+    c.out_off = (int64_t)out_off;
+    c.dst = a.out + out_off;
+    c.cap = out_cap > 0x7FFFFFFFu ? 0x7FFFFFFF : (int32_t)out_cap;
     c.dict = a.dict;
     c.dict_len = a.dict ? (int32_t)a.dict_len : 0;
     c.isolate = a.isolate;
@@ -1096,6 +1162,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     int32_t status = 0;
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
     bool have_pf = false;
+    Deferred dfr;                          // round 1's last piece batch, stored during the next parse
+    dfr.any = false;
     int64_t pf_at = -1;                    // compressed position pf0/pf1 were loaded from
 #if LZ4MI_PROFILE
     uint64_t prof[24] = {0};
@@ -1213,6 +1281,12 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (nE >= seg1) vis = 0;
         else vis &= ~((1u << (nE - seg0)) - 1u);
         tail = lane_of(x, kWave - 1);   // where the chain leaves the chunk
+        if (dfr.any) flush_deferred(c, dfr);   // the previous chunk's last pieces (their loads are back by now)
+#pragma unroll
+        for (int j = 0; j < kPieceBatch; ++j) {   // (the old values end here: not live through this chunk)
+            dfr.v[j] = make_uint4(0, 0, 0, 0);
+            dfr.y[j] = -1;
+        }
         if (tail > (uint32_t)kLim && tail < kEnd) tail = kStop;   // (fast table: raw positions past the window)
         }
         (void)seg1;
@@ -1412,22 +1486,37 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         uint32_t ready = 0;   // bit i: ... is written by this lane in this round
         uint32_t rbits = 0;   // bit i: ... reads a remapped source (SeqInfo::rsrc)
+        uint32_t nlit_pack = 0;   // byte i (rows < 4): literal prefix of a split match (remap_src 3)
         for (uint32_t i = 0; 64 * i < nseq; ++i) {            // round 1
             const uint32_t k = 64 * i + lane;
-            Run L = no_run(), M = no_run(), ML = no_run();
+            Run M = no_run(), ML = no_run();
+            SeqInfo q = seq_info(S, k < nseq ? k : 0u);
+            if (k >= nseq) q.ll = 0;
+            {   // the literal runs first (their registers are free before the remap)
+                const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
+                const bool longL = L.n > kLaneBytes;
+                lane_literals(c, S, longL ? no_run() : L);
+                for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
+            }
             if (k < nseq) {
-                const SeqInfo q = seq_info(S, k);
                 const int32_t t0 = q.out;
-                if (q.ll) L = Run{t0, q.ll, q.lit, 0, R_LDS};
                 M = match_run(c, t0 + q.ll, q.off, q.ml);
                 if (M.n == 0) {
                     M.kind = R_NONE;
                 } else if (match_src_end(M) > (int32_t)c.O) {
                     // the source is output of this table: map it back through the
                     // sequences that wrote it, else wait for a later round
-                    int32_t rs = M.src, re = match_src_end(M), li = 0;
-                    const int r = (M.kind == R_HIST && M.period == 0) ? remap_src(c, S, nseq, msh, rs, re, li) : 0;
-                    if (r == 1) {
+                    int32_t rs = M.src, re = match_src_end(M), li = 0, nl = 0;
+                    const int r = (M.kind == R_HIST && M.period == 0)
+                                      ? remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4)
+                                      : 0;
+                    if (r == 3) {   // literal prefix from the stage, the rest from finished output
+                        ML = Run{M.y, nl, li, 0, R_LDS};
+                        M.y += nl;
+                        M.n -= nl;
+                        nlit_pack |= (uint32_t)nl << (8 * i);
+                    }
+                    if (r == 1 || r == 3) {
                         M.src = rs;
                         if (c.out_off + rs < 16) M.kind = R_BYTES;
                         S.t_seq[k].w = (uint32_t)rs;
@@ -1441,22 +1530,23 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     }
                 }
             }
-            const bool longL = L.n > kLaneBytes, longM = M.kind != R_NONE && M.n > kLaneBytes;
+            const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
             const bool longML = ML.n > kLaneBytes;
             const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
             PROF(16);
-            lane_literals(c, S, longL ? no_run() : L);
             lane_literals(c, S, longML ? no_run() : ML);
             PROF(17);
             for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)), no_pat());
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
-            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_round1(S));
             PROF(18);
         }
 #if LZ4MI_PIECES
-        piece_pipe(c, S, ready, rbits, lane, nseq);
+        piece_pipe(c, S, ready, rbits, lane, nseq, dfr, LZ4MI_DEFER && !cut && !a.f1check && __ballot(pend != 0) == 0,
+                   nlit_pack);
+        if (dfr.any) goto chunk_done;   // nothing else to write (and the deferred batch stays out of
+                                        // the rounds' registers)
 #else
         {
             LaneMatchGen g{c, S, ready, rbits, lane, 0, 0, 0, 0, 0};
@@ -1511,7 +1601,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_rounds(S));
             }
 #if LZ4MI_PIECES
-            piece_pipe(c, S, ready, 0u, lane, nseq);
+            piece_pipe(c, S, ready, 0u, lane, nseq, dfr, false, 0u);
 #else
             {
                 LaneMatchGen g{c, S, ready, 0u, lane, 0, 0, 0, 0, 0};
@@ -1562,6 +1652,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             }
         }
 #endif
+    chunk_done:
         c.O = tab_hi;
         if (cut) {
             c.O += cll + cml;
@@ -1574,6 +1665,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         __syncthreads();
         PROF(8);
     }
+    if (dfr.any) flush_deferred(c, dfr);   // the last chunk's deferred pieces
 #if LZ4MI_PROFILE
     if (lane == 0)
         for (int i = 0; i < 24; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
