@@ -525,10 +525,17 @@ __device__ __forceinline__ void load_slots(const Ctx& c, const DecShared& S, con
 }
 
 template <bool TWO, int NB>
-__device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Slot (&s)[NB], const uint4 (&A)[NB],
-                                            const uint4 (&B)[NB]) {
+__device__ __forceinline__ void store_slots(const Ctx& c, DecShared& S, const Slot (&s)[NB], const uint4 (&A0)[NB],
+                                            const uint4 (&B0)[NB]) {
+    uint4 A[NB], B[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+        A[j] = A0[j];          // (consumed on every path: see lane_store)
+        settle(A[j]);
+        if (TWO) {
+            B[j] = B0[j];
+            settle(B[j]);
+        }
         const uint32_t mode = s[j].wm >> 8;
         if (!mode) continue;
         uint4 v = A[j];
@@ -695,9 +702,15 @@ __device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], ui
 }
 
 template <int NB>
-__device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A)[NB]) {
+__device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A0)[NB]) {
+    uint4 A[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+        // consumed on every path (a counted wait here): a load whose register is left
+        // pending on the paths that skip its store would make the next chunk's first write
+        // of that register wait for vmcnt(0) — for every store in flight
+        A[j] = A0[j];
+        settle(A[j]);
         if (!s[j].w) continue;
         if (LZ4MI_ABLATE == 4) {
             if ((A[j].x ^ A[j].y) == 0x9E3779B9u) S.pms[0] = 1;

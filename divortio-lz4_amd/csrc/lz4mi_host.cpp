@@ -144,3 +144,123 @@ int32_t lz4mi_host_compress_chain(const uint8_t* src, uint64_t src_total, int32_
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Host-CPU block decoder of the routing (a dependent-block frame decodes block by block,
+// each block reading the previous blocks' output: one serial chain). A fresh
+// restatement of decompressBlock (src/block/blockDecompress.js:30-275) with the reference's
+// typed-array semantics: reads past an array's end (or before its start) give 0, writes
+// past the output's end vanish, and — unless `spec` — the double-copy tail of a short far
+// match rewrites the bytes before it (:219-250). `spec` decodes per the LZ4
+// format instead (what every other LZ4 implementation writes).
+namespace {
+
+struct Arr {
+    const uint8_t* p;
+    int64_t n;
+    inline uint32_t at(int64_t i) const { return (i >= 0 && i < n) ? p[i] : 0u; }
+};
+
+struct OutArr {
+    uint8_t* p;
+    int64_t n;
+    inline uint32_t at(int64_t i) const { return (i >= 0 && i < n) ? p[i] : 0u; }
+    inline void put(int64_t i, uint32_t v) {
+        if (i >= 0 && i < n) p[i] = (uint8_t)v;
+    }
+};
+
+int64_t decompress_block(Arr in, int64_t in_pos, int64_t in_end, OutArr out, int64_t out_pos, Arr dict, bool spec) {
+    const int64_t out0 = out_pos;
+    while (in_pos < in_end) {
+        const uint32_t token = in.at(in_pos++);
+        int64_t ll = token >> 4;
+        if (ll == 15) {
+            uint32_t s;
+            do {
+                s = in.at(in_pos++);
+                ll += s;
+            } while (s == 255);
+        }
+        const int64_t end_lit = out_pos + ll;
+        if (end_lit > out.n) return LZ4MI_ERR_OUTPUT_TOO_SMALL;   // :74
+        if (in_pos + ll > in_end) return LZ4MI_ERR_MALFORMED;       // :75
+        if (ll > 0) {
+            if (in_pos >= 0 && in_pos + ll <= in.n) {
+                std::memcpy(out.p + out_pos, in.p + in_pos, (size_t)ll);
+            } else {
+                for (int64_t k = 0; k < ll; ++k) out.put(out_pos + k, in.at(in_pos + k));
+            }
+        }
+        out_pos = end_lit;
+        in_pos += ll;
+        if (in_pos >= in_end) break;
+        const uint32_t offset = in.at(in_pos) | (in.at(in_pos + 1) << 8);
+        in_pos += 2;
+        if (offset == 0) return LZ4MI_ERR_OFFSET0;                  // :128
+        int64_t ml = token & 15;
+        if (ml == 15) {
+            uint32_t s;
+            do {
+                s = in.at(in_pos++);
+                ml += s;
+            } while (s == 255);
+        }
+        ml += 4;
+        int64_t src = out_pos - (int64_t)offset;
+        if (src < 0) {                                              // dictionary (:143-185)
+            int64_t from_dict = -src;
+            src += dict.n;
+            if (from_dict > ml) from_dict = ml;
+            if (src < 0 || src + from_dict > dict.n) return LZ4MI_ERR_DICT_OOB;
+            for (int64_t k = 0; k < from_dict; ++k) out.put(out_pos + k, dict.p[src + k]);
+            out_pos += from_dict;
+            const int64_t rest = ml - from_dict;
+            for (int64_t k = 0; k < rest; ++k, ++out_pos) out.put(out_pos, out.at(out_pos - (int64_t)offset));
+            continue;
+        }
+        if (offset == 1) {                                          // output.fill (:190)
+            const uint32_t v = out.at(src);
+            const int64_t a = out_pos < out.n ? out_pos : out.n, b = out_pos + ml < out.n ? out_pos + ml : out.n;
+            if (b > a) std::memset(out.p + a, (int)v, (size_t)(b - a));
+            out_pos += ml;
+            continue;
+        }
+        if ((int64_t)offset >= ml && ml > 16) {                     // output.copyWithin (:195)
+            int64_t cnt = ml;
+            if (src + cnt > out.n) cnt = out.n - src;
+            if (out_pos + cnt > out.n) cnt = out.n - out_pos;
+            if (cnt > 0) std::memmove(out.p + out_pos, out.p + src, (size_t)cnt);
+            out_pos += ml;
+            continue;
+        }
+        const int64_t end = out_pos + ml;                           // general copy (:200-268)
+        if (offset >= 8 && !spec) {
+            int64_t r = src;
+            while (out_pos < end - 8) {
+                for (int k = 0; k < 8; ++k) out.put(out_pos + k, out.at(r + k));
+                out_pos += 8;
+                r += 8;
+            }
+            if (out_pos < end) {                                    // the double-copy tail (F1)
+                const int64_t t_out = end - 8, t_src = r + (end - out_pos) - 8;
+                for (int k = 0; k < 8; ++k) out.put(t_out + k, out.at(t_src + k));
+                out_pos = end;
+            }
+        } else {
+            for (int64_t r = src; out_pos < end; ++out_pos, ++r) out.put(out_pos, out.at(r));
+        }
+    }
+    return (int64_t)(int32_t)(out_pos - out0);
+}
+
+}  // namespace
+
+extern "C" int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_total, int64_t in_off, int64_t in_size,
+                                               uint8_t* out, uint64_t out_total, int64_t out_off, const uint8_t* dict,
+                                               uint32_t dict_len, uint32_t flags) {
+    if ((!in && in_total) || (!out && out_total) || (!dict && dict_len) || in_off < 0 || in_size < 0 || out_off < 0)
+        return LZ4MI_ERR_ARG;
+    return decompress_block(Arr{in, (int64_t)in_total}, in_off, in_off + in_size, OutArr{out, (int64_t)out_total},
+                            out_off, Arr{dict, (int64_t)dict_len}, !(flags & (LZ4MI_JS_COMPAT | LZ4MI_JS_EXACT)));
+}

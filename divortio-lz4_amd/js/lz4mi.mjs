@@ -334,19 +334,25 @@ export function decompress(input, dictionary = null, verifyChecksum = true, veri
         }
     }
 
+    // Routing: a frame of dependent blocks (FLG bit 0x20 clear) is one serial chain — each
+    // block reads its predecessors' output — so its blocks go through the addon's host
+    // decoder in order; independent blocks are decoded on the GPU in one batch.
+    const independent = (flg & 0x20) !== 0;
+    if (!independent) requireDevice();
+    const decodeBlock = independent ? native.decompressBlock : native.decompressBlockHost;
     let result;
     if (expected > 0) {
         result = new Uint8Array(expected);
         const dict = dictionary || null;
-        if (!batchDirect(data, blocks, result, dict, BLOCK_MAX_SIZES[(bd >> 4) & 7] || 4194304)) {
-            result.fill(0);      // forget whatever the batch attempt wrote
+        if (!independent || !batchDirect(data, blocks, result, dict, BLOCK_MAX_SIZES[(bd >> 4) & 7] || 4194304)) {
+            if (independent) result.fill(0);      // forget whatever the batch attempt wrote
             let rp = 0;
             for (const b of blocks) {
                 if (b.raw) {
                     result.set(data.subarray(b.pos, b.pos + b.n), rp);
                     rp += b.n;           // the reference advances by the declared size
                 } else {
-                    rp += native.decompressBlock(data, b.pos, b.n, result, rp, dict, decodeFlags);
+                    rp += decodeBlock(data, b.pos, b.n, result, rp, dict, decodeFlags);
                 }
             }
         }
@@ -365,7 +371,7 @@ export function decompress(input, dictionary = null, verifyChecksum = true, veri
             if (b.raw) {
                 chunk = data.slice(b.pos, b.pos + b.n);
             } else {
-                const w = native.decompressBlock(data, b.pos, b.n, workspace, 0,
+                const w = decodeBlock(data, b.pos, b.n, workspace, 0,
                     wpos > 0 ? window.subarray(0, wpos) : null, decodeFlags);
                 chunk = workspace.slice(0, w);
             }

@@ -39,7 +39,7 @@ EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_ve
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
            "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
            "lz4mi_frame_decompress", "lz4mi_frame_index", "lz4mi_compress_chain",
-           "lz4mi_host_compress_block", "lz4mi_host_compress_chain")
+           "lz4mi_host_compress_block", "lz4mi_host_compress_chain", "lz4mi_host_decompress_block")
 
 
 class Lz4miError(RuntimeError):
@@ -103,6 +103,9 @@ def lib():
         L.lz4mi_host_compress_chain.restype = ctypes.c_int32
         L.lz4mi_host_compress_chain.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                 _vp, _vp, _vp, _vp]
+        L.lz4mi_host_decompress_block.restype = ctypes.c_int64
+        L.lz4mi_host_decompress_block.argtypes = [_vp, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, _vp,
+                                                  ctypes.c_uint64, ctypes.c_int64, _vp, ctypes.c_uint32, ctypes.c_uint32]
         L.lz4mi_frame_index.restype = ctypes.c_int32
         L.lz4mi_frame_index.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
@@ -236,6 +239,21 @@ def compress_chain(src, start, length, block_size, hash_table, host=False):
         _check(lib().lz4mi_compress_chain(_p(s), s.size, start, length, block_size, hash_table.ctypes.data,
                                           _p(out), _p(out_off), _p(comp_len), 0, None))
     return [out[int(o):int(o) + int(n)].copy() for o, n in zip(out_off, comp_len)]
+
+
+def host_decompress_raw(inp, input_offset, input_size, output, output_offset=0, dictionary=None, spec=False):
+    """decompressBlock on the host decoder (lz4mi_host_decompress_block): writes into `output`
+    (numpy uint8, the whole output array) and returns bytes written; raises with the reference's
+    message. Reference bytes (F1 included) unless `spec`."""
+    a = _u8(inp)
+    d = None if dictionary is None else _u8(dictionary)
+    assert output.dtype == np.uint8 and output.flags.c_contiguous
+    r = lib().lz4mi_host_decompress_block(_p(a), a.size, input_offset, input_size, _p(output), output.size,
+                                          output_offset, None if d is None else _p(d), 0 if d is None else d.size,
+                                          0 if spec else JS_EXACT)
+    if r < 0:
+        raise Lz4miError(int(r))
+    return int(r)
 
 
 def host_compress_raw(src, output, src_start, src_len, hash_table, output_offset):

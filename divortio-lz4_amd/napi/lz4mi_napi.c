@@ -155,8 +155,10 @@ static napi_value n_compress_block_host(napi_env env, napi_callback_info info) {
     return compress_block_impl(env, info, 1);
 }
 
-/* decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary) */
-static napi_value n_decompress_block(napi_env env, napi_callback_info info) {
+/* decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary) on the GPU;
+ * decompressBlockHost: the same on the host decoder (lz4mi_host_decompress_block, the JS
+ * layer's route for the blocks of dependent-block frames) */
+static napi_value decompress_block_impl(napi_env env, napi_callback_info info, int host) {
     size_t argc = 7;
     napi_value argv[7];
     CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
@@ -172,6 +174,13 @@ static napi_value n_decompress_block(napi_env env, napi_callback_info info) {
         return throw_status(env, LZ4MI_ERR_MALFORMED);
     }
     if (o0 < 0 || (uint64_t)o0 > out.length) return throw_status(env, LZ4MI_ERR_OUTPUT_TOO_SMALL);
+    if (host) {
+        int64_t r = lz4mi_host_decompress_block((const uint8_t*)in.data, in.length, i0, n, (uint8_t*)out.data,
+                                                out.length, o0, (const uint8_t*)dict.data, (uint32_t)dict.length,
+                                                (uint32_t)flags);
+        if (r < 0) return throw_status(env, r);
+        return make_i64(env, r);
+    }
     uint64_t in_off = (uint64_t)i0, out_off = (uint64_t)o0;
     uint32_t in_len = (uint32_t)n, out_cap = (uint32_t)(out.length - out_off), out_len = 0;
     int32_t status = 0;
@@ -181,6 +190,11 @@ static napi_value n_decompress_block(napi_env env, napi_callback_info info) {
     if (st) return throw_status(env, st);
     if (status) return throw_status(env, status);
     return make_i64(env, out_len);
+}
+
+static napi_value n_decompress_block(napi_env env, napi_callback_info info) { return decompress_block_impl(env, info, 0); }
+static napi_value n_decompress_block_host(napi_env env, napi_callback_info info) {
+    return decompress_block_impl(env, info, 1);
 }
 
 /* Block offsets: a Float64Array whose entries are integers in [0, 2^53) (anything else
@@ -501,6 +515,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"compressChain", NULL, n_compress_chain, NULL, NULL, NULL, napi_default, NULL},
         {"compressBlockHost", NULL, n_compress_block_host, NULL, NULL, NULL, napi_default, NULL},
         {"compressChainHost", NULL, n_compress_chain_host, NULL, NULL, NULL, napi_default, NULL},
+        {"decompressBlockHost", NULL, n_decompress_block_host, NULL, NULL, NULL, napi_default, NULL},
         {"decompressBlocks", NULL, n_decompress_blocks, NULL, NULL, NULL, napi_default, NULL},
         {"xxHash32", NULL, n_xxh32, NULL, NULL, NULL, napi_default, NULL},
         {"xxh32Reset", NULL, n_xxh32_reset, NULL, NULL, NULL, napi_default, NULL},

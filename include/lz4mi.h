@@ -232,6 +232,18 @@ int64_t lz4mi_host_compress_block(const uint8_t* src, uint64_t src_total, int32_
 int32_t lz4mi_host_compress_chain(const uint8_t* src, uint64_t src_total, int32_t start, int32_t len,
                                   int32_t block_size, int32_t* table, uint8_t* out, const uint64_t* out_off,
                                   uint32_t* comp_len);
+/*
+ * Host-CPU block decoder of the same routing: decompressBlock(input, inputOffset, inputSize,
+ * output, outputOffset, dictionary) (src/block/blockDecompress.js:30-275) on the calling thread,
+ * for blocks that read their predecessors' output (dependent-block frames, decoded in order).
+ * in[0 .. in_total) is the whole input array, out[0 .. out_total) the whole output array
+ * (positions absolute in it; below 0 the tail of dict). flags & (LZ4MI_JS_EXACT | LZ4MI_JS_COMPAT):
+ * the reference's bytes, its double-copy-tail rewrite included; else LZ4 spec.
+ * Returns bytes written (outPos - outputOffset) or a negative status with the reference's meaning.
+ */
+int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_total, int64_t in_off, int64_t in_size,
+                                    uint8_t* out, uint64_t out_total, int64_t out_off, const uint8_t* dict,
+                                    uint32_t dict_len, uint32_t flags);
 
 /*
  * Block index of a device-resident frame, for decoding its blocks on several devices

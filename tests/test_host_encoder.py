@@ -102,3 +102,70 @@ def test_host_digest_manifest_4mib(manifest, kind):
     for r in [r for r in g["rows"] if r["gen"] == kind][:4]:
         comp = _host_block(O.generate(kind, r["seed"], r["n"]))
         assert comp.size == r["comp_len"] and "%08x" % lz4mi.xxh32(comp) == r["comp_xxh"], r
+
+
+# ---- the host decoder of the same routing (lz4mi_host_decompress_block) ----------------
+
+MESSAGES = {-1: "LZ4: Output Buffer Too Small", -2: "LZ4: Malformed Input", -3: "LZ4: Invalid Offset 0",
+            -4: "LZ4: Dictionary Offset Out of Bounds"}
+
+
+def test_host_decoder_reference_blocks(manifest):
+    """Every golden block decoded with the reference's semantics: its written count and its
+    bytes (the reference decoder's own output, F1 corruption included), and in spec mode the
+    input back."""
+    for c in cases_of(manifest, "block"):
+        src = _src_of(c)
+        comp = golden_bytes(c["comp_file"]) if c["comp_file"] else _host_block(src)
+        out = np.zeros(src.size, dtype=np.uint8)
+        w = lz4mi.host_decompress_raw(comp, 0, comp.size, out, 0)
+        assert w == c["js_dec_written"], c["name"]
+        if c["js_dec_equals_input"]:
+            assert np.array_equal(out, src), c["name"]
+        else:
+            assert "%08x" % lz4mi.xxh32(out) == c["js_dec_xxh"], c["name"]
+        spec = np.zeros(src.size, dtype=np.uint8)
+        assert lz4mi.host_decompress_raw(comp, 0, comp.size, spec, 0, spec=True) == src.size
+        assert np.array_equal(spec, src), c["name"]
+
+
+def test_host_decoder_edge_and_error_cases(manifest):
+    """The reference decoder's own results on the edge / corruption vectors: bytes, counts,
+    dictionary reads, and the four error messages in its check order."""
+    (g,) = cases_of(manifest, "decode_cases")
+    for c in g["cases"]:
+        comp = np.array(c["comp"], dtype=np.uint8)
+        dic = None if c["dict"] is None else np.array(c["dict"], dtype=np.uint8)
+        out = np.zeros(c["out_len"], dtype=np.uint8)
+        try:
+            w = lz4mi.host_decompress_raw(comp, 0, comp.size, out, c["out_off"], dictionary=dic)
+            assert c["ok"] and w == c["written"] and out.tolist() == c["out"], c["name"]
+        except lz4mi.Lz4miError as e:
+            assert not c["ok"] and MESSAGES.get(e.status) == c["error"], (c["name"], e.status)
+
+
+def test_host_decoder_dependent_frames(manifest):
+    """The golden dependent-block frames (one table carried, blocks reading earlier blocks'
+    output) decoded block by block in order by the host decoder into one result buffer, as
+    bufferDecompress.js does with a content size: the reference's decoded bytes."""
+    (g,) = cases_of(manifest, "frames")
+    from lz4mi import shard
+    done = 0
+    for f in g["frames"]:
+        if f["indep"] or not f.get("frame_file") or "dict" in f or "dict_text" in f or not f.get("dec_ok"):
+            continue
+        fr = golden_bytes(f["frame_file"])
+        info, blocks = shard.frame_blocks(fr)
+        if info["content_size"] <= 0:
+            continue
+        out = np.zeros(info["content_size"], dtype=np.uint8)
+        pos = 0
+        for p, n, stored in blocks:
+            if stored:
+                out[pos:pos + n] = fr[p:p + n]
+                pos += n
+            else:
+                pos += lz4mi.host_decompress_raw(fr, p, n, out, pos)
+        assert pos == f["dec_len"] and "%08x" % lz4mi.xxh32(out[:pos]) == f["dec_xxh"], f
+        done += 1
+    assert done >= 4

@@ -2,8 +2,9 @@
 // kernels + D2H + JS frame assembly), as a caller of the reference's API sees them.
 //   node tools/napi_e2e.mjs <input file> [reps] [dependent-mode bytes]
 // Prints one JSON line: LZ4.compress with independent blocks (batched), LZ4.compress
-// with the reference's default dependent blocks (one GPU call per block, the table
-// carried), LZ4.decompress in 'spec' and 'reference' (default) modes.
+// with the reference's default dependent blocks (the layer's host route: one serial chain,
+// the table carried; checked to decode back), LZ4.decompress in 'spec' and 'reference'
+// (default) modes, and the decode of the dependent frame.
 import fs from 'fs';
 import { LZ4 } from '../divortio-lz4_amd/js/lz4mi.mjs';
 
@@ -22,8 +23,13 @@ let frame = LZ4.compress(input, null, 4194304, true, false);
 out.ratio = +(input.length / frame.length).toFixed(3);
 out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, 4194304, true, false); }, reps);
 const dep = input.subarray(0, depBytes);
-out.compress_dependent_default_GBps = rate(dep.length, () => LZ4.compress(dep), 1);
+let depFrame = null;
+out.compress_dependent_default_GBps = rate(dep.length, () => { depFrame = LZ4.compress(dep); }, 1);
 out.dependent_bytes = dep.length;
+LZ4.setDecodeMode('spec');
+if (Buffer.compare(Buffer.from(LZ4.decompress(depFrame)), Buffer.from(dep)) !== 0)
+    throw new Error('dependent frame round trip mismatch');
+out.decompress_dependent_GBps = rate(dep.length, () => LZ4.decompress(depFrame), 1);
 for (const mode of ['spec', 'reference']) {
     LZ4.setDecodeMode(mode);
     const back = LZ4.decompress(frame);
