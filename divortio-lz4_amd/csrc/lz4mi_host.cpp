@@ -235,6 +235,28 @@ int64_t decompress_block(Arr in, int64_t in_pos, int64_t in_end, OutArr out, int
             continue;
         }
         const int64_t end = out_pos + ml;                           // general copy (:200-268)
+        if (end <= out.n && src >= 0) {                             // in bounds: no per-byte checks
+            uint8_t* o = out.p;
+            if (offset >= 8) {
+                int64_t r = src;
+                for (; out_pos + 8 <= end; out_pos += 8, r += 8) std::memcpy(o + out_pos, o + r, 8);
+                if (out_pos < end) {
+                    if (spec) {
+                        for (; out_pos < end; ++out_pos, ++r) o[out_pos] = o[r];
+                    } else if (end - 8 >= 0) {                      // F1: the last 8 bytes again
+                        std::memcpy(o + end - 8, o + r + (end - out_pos) - 8, 8);
+                        out_pos = end;
+                    } else {
+                        const int64_t t_out = end - 8, t_src = r + (end - out_pos) - 8;
+                        for (int k = 0; k < 8; ++k) out.put(t_out + k, out.at(t_src + k));
+                        out_pos = end;
+                    }
+                }
+            } else {
+                for (int64_t r = src; out_pos < end; ++out_pos, ++r) o[out_pos] = o[r];
+            }
+            continue;
+        }
         if (offset >= 8 && !spec) {
             int64_t r = src;
             while (out_pos < end - 8) {
