@@ -388,33 +388,47 @@ def reference_benchmark(with_js):
 
 
 def single_block(torch, lz4mi, batch, reps=5):
-    """One 4 MiB block through the raw-block C-ABI with host buffers (LZ4.compressRaw /
-    LZ4.decompressRaw: lz4mi_compress_block_table — the chain kernel with the caller's table
-    in LDS — and lz4mi_decompress_blocks with nblocks = 1), PCIe included, median of `reps`
-    calls; the host encoder (lz4mi_host_compress_block, the layer's route for serial-chain
-    calls) beside it. Latency, not throughput: one block is one wave."""
+    """Raw-block calls through the C-ABI with host buffers (LZ4.compressRaw / LZ4.decompressRaw:
+    lz4mi_compress_block_table — the chain kernel with the caller's table in LDS — and
+    lz4mi_decompress_blocks with nblocks = 1), PCIe included, median of `reps` calls, beside the
+    host encoder/decoder (lz4mi_host_compress_block / lz4mi_host_decompress_block, the layer's
+    route for serial-chain calls) on the same bytes, at 64 KiB, 1 MiB and 4 MiB (prefixes of one
+    tiles216 block): the GPU/host crossover of DESIGN §5. Latency, not throughput: one block is
+    one wave."""
     import numpy as np
-    src = batch.raw[:BLOCK].cpu().numpy()
-    out = np.zeros(lz4mi.compress_bound(BLOCK), dtype=np.uint8)
-    res = {}
-    for name, fn in (("compressRaw_gpu", lz4mi.compress_raw), ("compressRaw_host", lz4mi.host_compress_raw)):
+    src_all = batch.raw[:BLOCK].cpu().numpy()
+
+    def med(fn):
         ts = []
         for _ in range(reps):
-            t = np.zeros(16384, dtype=np.int32)
             t0 = time.perf_counter()
-            n = fn(src, out, 0, BLOCK, t, 0)
+            r = fn()
             ts.append(time.perf_counter() - t0)
-        res[name + "_ms"] = round(sorted(ts)[len(ts) // 2] * 1e3, 3)
-    comp = out[:n].copy()
-    dec = np.zeros(BLOCK, dtype=np.uint8)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        w = lz4mi.decompress_raw(comp, 0, comp.size, dec, 0)
-        ts.append(time.perf_counter() - t0)
-    res["decompressRaw_gpu_ms"] = round(sorted(ts)[len(ts) // 2] * 1e3, 3)
-    res["verified"] = bool(w == BLOCK and np.array_equal(dec, src))
-    res["workload"] = "one 4 MiB block of the bench's tiles216 batch, host buffers, fresh table, median of %d calls" % reps
+        return r, round(sorted(ts)[len(ts) // 2] * 1e3, 3)
+
+    res, ok = {}, True
+    for size in (65536, 1 << 20, BLOCK):
+        src = np.ascontiguousarray(src_all[:size])
+        out = np.zeros(lz4mi.compress_bound(size), dtype=np.uint8)
+        row, comp = {}, None
+        for name, fn in (("compressRaw_gpu", lz4mi.compress_raw), ("compressRaw_host", lz4mi.host_compress_raw)):
+            n, row[name + "_ms"] = med(lambda: fn(src, out, 0, size, np.zeros(16384, dtype=np.int32), 0))
+            if comp is None:
+                comp = out[:n].copy()
+            ok &= bool(np.array_equal(out[:n], comp))
+        dec = np.zeros(size, dtype=np.uint8)
+        for name, fn in (("decompressRaw_gpu", lambda: lz4mi.decompress_raw(comp, 0, comp.size, dec, 0)),
+                         ("decompressRaw_host", lambda: lz4mi.host_decompress_raw(comp, 0, comp.size, dec, 0))):
+            dec[:] = 0
+            w, row[name + "_ms"] = med(fn)
+            ok &= bool(w == size and np.array_equal(dec, src))
+        if size == BLOCK:
+            res.update(row)
+        else:
+            res["%d_KiB" % (size >> 10)] = row
+    res["verified"] = ok
+    res["workload"] = ("one tiles216 block of the bench's batch (and its 64 KiB / 1 MiB prefixes), host buffers, "
+                       "fresh table, median of %d calls" % reps)
     return res
 
 

@@ -80,15 +80,39 @@ function blockId(bytes) {             // bufferCompress.js:77-82
     return 7;
 }
 
-/** compressBlock (src/block/blockCompress.js:31) on the GPU. */
+// Routing (SURVEY.md §8b, DESIGN §5 "Routing"). A batch of b independent blocks costs the GPU
+// about one block's chain latency (every block is one wave, all resident at once) and the host
+// b blocks one after another, so the GPU wins from a block count on that is nearly independent
+// of the block size: the crossovers below are the single-block latencies measured on the box
+// (bench.py `single_block`). A raw-block call is one block: the host's. 'gpu' sends every
+// call to the kernels (tests; the kernels' own parity).
+const HOST_MAX_BLOCKS_COMPRESS = 16;     // tiles216 4 MiB: GPU batch ~45 ms vs host ~3 ms per block
+const HOST_MAX_BLOCKS_DECOMPRESS = 4;    // GPU batch ~5 ms incl. PCIe vs host ~1.2 ms per block
+let routing = 'auto';
+
+/** 'auto' (default: the measured crossovers above) or 'gpu' (every block call on the GPU). */
+export function setRouting(mode) {
+    if (mode !== 'auto' && mode !== 'gpu') throw new TypeError("lz4mi: routing must be 'auto' or 'gpu'");
+    routing = mode;
+}
+
+const hostRoute = (nblocks, max) => {
+    if (routing !== 'auto' || nblocks > max) return false;
+    requireDevice();
+    return true;
+};
+
+/** compressBlock (src/block/blockCompress.js:31): one serial chain, the host encoder unless routing 'gpu'. */
 export function compressRaw(src, output, srcStart, srcLen, hashTable, outputOffset) {
+    if (hostRoute(1, HOST_MAX_BLOCKS_COMPRESS))
+        return native.compressBlockHost(src, output, srcStart, srcLen, hashTable, outputOffset);
     return native.compressBlock(src, output, srcStart, srcLen, hashTable, outputOffset);
 }
 
-/** decompressBlock (src/block/blockDecompress.js:30) on the GPU. */
+/** decompressBlock (src/block/blockDecompress.js:30): one block, the host decoder unless routing 'gpu'. */
 export function decompressRaw(input, inputOffset, inputSize, output, outputOffset, dictionary) {
-    return native.decompressBlock(input, inputOffset, inputSize, output, outputOffset, dictionary || null,
-        decodeFlags);
+    const f = hostRoute(1, HOST_MAX_BLOCKS_DECOMPRESS) ? native.decompressBlockHost : native.decompressBlock;
+    return f(input, inputOffset, inputSize, output, outputOffset, dictionary || null, decodeFlags);
 }
 
 /**
@@ -225,7 +249,15 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
             pos += n;
         }
         const nb = Math.ceil((end - pos) / bsize);
-        if (nb > 0) {
+        if (nb > 0 && hostRoute(nb, HOST_MAX_BLOCKS_COMPRESS)) {
+            const scratch = new Uint8Array(bsize + ((bsize / 255) | 0) + 16);
+            for (; pos < end; pos += bsize) {
+                const n = Math.min(bsize, end - pos);
+                table.fill(0);
+                const c = native.compressBlockHost(work, scratch, pos, n, table, 0);
+                emit(pos, n, c, scratch.subarray(0, Math.max(0, Math.min(c, scratch.length))));
+            }
+        } else if (nb > 0) {
             const srcOff = new Float64Array(nb), srcLen = new Uint32Array(nb);
             const outOff = new Float64Array(nb), outLen = new Uint32Array(nb);
             let slot = 0;
@@ -244,10 +276,25 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
     } else {
         // Dependent blocks (the reference's default): one table carried across blocks, each
         // block exactly compressBlock(work, scratch, pos, n, table, 0), the table updated in
-        // place — one serial chain, so the host route (compressChain would run it as one GPU
+        // place — one serial chain, so the host route (the chain kernel runs it as one GPU
         // wave: 0.12 GB/s on tiles216 against ~1.5 GB/s for the host encoder, DESIGN §5).
         const nb = Math.ceil((end - pos) / bsize);
-        if (nb > 0) {
+        if (nb > 0 && routing === 'gpu') {
+            let slot = 0;
+            const outOff = new Float64Array(nb), compLen = new Uint32Array(nb);
+            for (let b = 0; b < nb; b++) {
+                const n = Math.min(bsize, end - pos - b * bsize);
+                outOff[b] = slot;
+                slot += n + ((n / 255) | 0) + 16;
+            }
+            const scratch = new Uint8Array(slot);
+            native.compressChain(work, pos, end - pos, bsize, table, scratch, outOff, compLen);
+            for (let b = 0; b < nb; b++) {
+                const n = Math.min(bsize, end - pos);
+                emit(pos, n, compLen[b], scratch.subarray(outOff[b], outOff[b] + compLen[b]));
+                pos += n;
+            }
+        } else if (nb > 0) {
             const outOff = new Float64Array(nb), compLen = new Uint32Array(nb);
             let slot = 0;
             for (let b = 0; b < nb; b++) {
@@ -338,14 +385,17 @@ export function decompress(input, dictionary = null, verifyChecksum = true, veri
     // block reads its predecessors' output — so its blocks go through the addon's host
     // decoder in order; independent blocks are decoded on the GPU in one batch.
     const independent = (flg & 0x20) !== 0;
-    if (!independent) requireDevice();
-    const decodeBlock = independent ? native.decompressBlock : native.decompressBlockHost;
+    let ncomp = 0;
+    for (const b of blocks) if (!b.raw) ncomp++;
+    const host = routing === 'auto' && (!independent || ncomp <= HOST_MAX_BLOCKS_DECOMPRESS);
+    if (host) requireDevice();
+    const decodeBlock = host ? native.decompressBlockHost : native.decompressBlock;
     let result;
     if (expected > 0) {
         result = new Uint8Array(expected);
         const dict = dictionary || null;
-        if (!independent || !batchDirect(data, blocks, result, dict, BLOCK_MAX_SIZES[(bd >> 4) & 7] || 4194304)) {
-            if (independent) result.fill(0);      // forget whatever the batch attempt wrote
+        if (host || !batchDirect(data, blocks, result, dict, BLOCK_MAX_SIZES[(bd >> 4) & 7] || 4194304)) {
+            if (!host) result.fill(0);            // forget whatever the batch attempt wrote
             let rp = 0;
             for (const b of blocks) {
                 if (b.raw) {
@@ -570,7 +620,15 @@ export class LZ4Encoder {
             slot += sizes[b] + ((sizes[b] / 255) | 0) + 16;
         }
         const scratch = new Uint8Array(slot);
-        native.compressBlocks(this.buffer, srcOff, srcLen, scratch, outOff, outLen);
+        if (hostRoute(nb, HOST_MAX_BLOCKS_COMPRESS)) {
+            const t = new Int32Array(HASH_TABLE_SIZE);
+            for (let b = 0; b < nb; b++) {
+                t.fill(0);
+                outLen[b] = native.compressBlockHost(this.buffer, scratch.subarray(outOff[b]), srcOff[b], srcLen[b], t, 0);
+            }
+        } else {
+            native.compressBlocks(this.buffer, srcOff, srcLen, scratch, outOff, outLen);
+        }
         const out = [];
         for (let b = 0; b < nb; b++) {
             const k = sizes[b], c = outLen[b];
@@ -605,7 +663,7 @@ export class LZ4Encoder {
         }
         const srcStart = this.dictSize;
         const output = new Uint8Array(blockSize + 1024 + 4);
-        const compSize = native.compressBlock(this.buffer, output, srcStart, blockSize, this.hashTable, 4);
+        const compSize = compressRaw(this.buffer, output, srcStart, blockSize, this.hashTable, 4);   // one chain
         let rec;
         if (compSize > 0 && compSize < blockSize) {
             writeU32(output, compSize, 0);
@@ -757,8 +815,8 @@ export class LZ4Decoder {
                     } else {
                         const dict = this.windowPos === WINDOW_SIZE ? this.window : this.window.subarray(0, this.windowPos);
                         const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
-                        const w = native.decompressBlock(blockData, 0, blockData.length, ws, 0,
-                            this.blockIndependence ? null : dict, decodeFlags);
+                        const w = decompressRaw(blockData, 0, blockData.length, ws, 0,
+                            this.blockIndependence ? null : dict);
                         dec = ws.slice(0, w);
                     }
                     output.push(dec);
@@ -790,6 +848,12 @@ export class LZ4Decoder {
     // (OUTPUT_TOO_SMALL) is decoded again alone into the reference's 4 MiB workspace below
     _decodeIndependent(blocks) {
         const nb = blocks.length, cap = this.blockMax || BLOCK_MAX_SIZES[7];
+        if (hostRoute(nb, HOST_MAX_BLOCKS_DECOMPRESS)) {
+            return blocks.map((b) => {
+                const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
+                return ws.slice(0, native.decompressBlockHost(b.data, 0, b.data.length, ws, 0, null, decodeFlags));
+            });
+        }
         let total = 0;
         for (const b of blocks) total += b.data.length;
         const input = new Uint8Array(total);
@@ -857,6 +921,7 @@ export const LZ4 = {
     LZ4Encoder,
     LZ4Decoder,
     setDecodeMode,
+    setRouting,
     version: native.version,
     buildId: native.buildId,
 };

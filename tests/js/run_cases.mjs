@@ -5,6 +5,7 @@ import fs from 'fs';
 import { LZ4 } from '../../divortio-lz4_amd/js/lz4mi.mjs';
 
 const job = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+LZ4.setRouting(process.argv[3] || 'gpu');   // 'gpu': every block call on the kernels; 'auto': the layer's routing
 const hex = (v) => (v >>> 0).toString(16).padStart(8, '0');
 const read = (p) => (p ? new Uint8Array(fs.readFileSync(p)) : null);
 const fromHex = (s) => Uint8Array.from(Buffer.from(s, 'hex'));
