@@ -65,7 +65,7 @@ __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
 }
 
 #ifndef LZ4MI_SHFL_READLANE
-#define LZ4MI_SHFL_READLANE 1   // 0: the two per-batch lane gathers as LDS permutes (A/B switch)
+#define LZ4MI_SHFL_READLANE 0   // 1: the two per-batch lane gathers as v_readlane (measured slower: SGPR spills)
 #endif
 
 // Lanes 8g .. 8g+7 get v of lane g (g < 8): eight v_readlane, no LDS permute round trip.
