@@ -46,6 +46,9 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#ifndef LZ4MI_PER_ALIGN
+#define LZ4MI_PER_ALIGN 0   // 1: long periodic runs stored on the 16-byte grid (A/B switch)
+#endif
 #endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
@@ -939,6 +942,28 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
         }
         __syncthreads();
         // every piece whose phase falls in this slice; the phase is carried from piece to piece
+#if LZ4MI_PER_ALIGN
+        // pieces on the absolute 16-byte grid (whole-line stores), the unaligned head piece
+        // written once more by lane 0 (same bytes), the last piece overlapping its predecessor
+        const int32_t a0 = (int32_t)((0u - (uint32_t)(uintptr_t)(c.dst + R.y)) & 15u);
+        if (lane == 0 && a0) {
+            const int32_t ph = 0 - s0;
+            if ((uint32_t)ph < (uint32_t)(e0 - s0)) out16(c.dst + R.y, stage16(B.w, ph));
+        }
+        const int32_t np = (R.n - a0 + 15) >> 4;
+        const int32_t step = (16 * kWave) % per;
+        int32_t r = (a0 + 16 * lane) % per;
+#pragma unroll 2
+        for (int32_t p = lane; p < np; p += kWave) {
+            const int32_t d0 = a0 + 16 * p;
+            const bool last = d0 > dl;
+            const int32_t d = last ? dl : d0;
+            const int32_t ph = (last ? d % per : r) - s0;
+            if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, ph));
+            r += step;
+            if (r >= per) r -= per;
+        }
+#else
         const int32_t np = run_pieces(R.n);
         const int32_t step = (16 * kWave) % per;
         int32_t r = (16 * lane) % per;
@@ -951,6 +976,7 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
             r += step;
             if (r >= per) r -= per;
         }
+#endif
     }
     __syncthreads();
 }
