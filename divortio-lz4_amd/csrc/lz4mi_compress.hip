@@ -484,19 +484,11 @@ __device__ __forceinline__ uint32_t first_nz16(uint4 x) {
 
 constexpr int32_t kWinBytes = 2048;   // source window in LDS: the probes' 4-byte reads
 
-#ifndef LZ4MI_BULK_EMIT
-#define LZ4MI_BULK_EMIT 0   // 1: accepted sequences listed in LDS and emitted 64 at a time, one per lane (A/B switch)
-#endif
-constexpr int kListMax = 64;
-
 struct GtsShared {
     uint8_t ring[2048];                  // output ring (half the batch encoder's: the window takes the rest)
     uint8_t slot[1024];                  // miss batches: lane ids keyed by hash & 1023
     uint32_t code[kCodeWords];           // 2-bit epoch code per table entry
     uint32_t win[kWinBytes / 4 + 4];     // source bytes [wb, wb + kWinBytes)
-#if LZ4MI_BULK_EMIT
-    int32_t lp[kListMax], lo[kListMax], le[kListMax];   // listed sequences: position, offset, match end
-#endif
 };
 
 __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T, int lane) {
@@ -604,70 +596,6 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
         }
     };
-#if LZ4MI_BULK_EMIT
-    // Accepted sequences are listed (lanes < k append theirs) and written 64 at a time, one
-    // sequence per lane: sizes by a wave scan, then every lane writes its token, literals (one
-    // 16-byte load per lane with literals), offset and length byte in one uniform byte loop.
-    // A list holding a general sequence (15+ literals, length field of 2+ extra bytes) goes out
-    // one sequence at a time.
-    int lcnt = 0;
-    auto list_add = [&](int k, int32_t p_, int32_t c_, int32_t e_) {
-        if (lane < k) {
-            F.lp[lcnt + lane] = p_;
-            F.lo[lcnt + lane] = p_ - c_;
-            F.le[lcnt + lane] = e_;
-        }
-        lcnt += k;
-    };
-    auto emit_list = [&]() {
-        const bool mine = lane < lcnt;
-        int32_t lp = 0, lof = 0, le = 0;
-        if (mine) {
-            lp = F.lp[lane];
-            lof = F.lo[lane];
-            le = F.le[lane];
-        }
-        const int32_t pe = (int32_t)dpp<kWaveShr1>((uint32_t)anchor, (uint32_t)le);   // previous sequence's end
-        const int32_t lit = lp - pe, mcode = le - lp - 4;
-        if (__ballot(mine && (lit >= 15 || mcode >= 15 + 255))) {
-            for (int k = 0; k < lcnt; ++k) {
-                const int32_t pm = lane_val(lp, k), e = lane_val(le, k);
-                emit_seq(F, o, j, lane, anchor, pm, (uint32_t)lane_val(lof, k), e - pm - 4);
-                anchor = e;
-            }
-            lcnt = 0;
-            return;
-        }
-        const uint32_t size = mine ? 3u + (uint32_t)lit + (mcode >= 15 ? 1u : 0u) : 0u;
-        const uint32_t incl = wave_incl_scan(size, lane);
-        const int32_t total = (int32_t)lane_val(incl, lcnt - 1);
-        const bool hl = mine && lit > 0;
-        uint4 lv = make_uint4(0, 0, 0, 0);
-        if (__ballot(hl)) {
-            if (hl) lv = ld16(j, pe);
-            wait_vmem();
-        }
-        settle32(lv.x); settle32(lv.y); settle32(lv.z); settle32(lv.w);
-        ring_reserve(F, o, lane, total);
-        const uint32_t at = (uint32_t)o.op + incl - size;
-        const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
-        for (uint32_t t = 0; __ballot(t < size); ++t) {
-            if (t < size) {
-                uint32_t v;
-                const uint32_t q = t - 1;
-                if (t == 0) v = tok;
-                else if ((int32_t)t <= lit) v = ((q < 8 ? (q < 4 ? lv.x : lv.y) : (q < 12 ? lv.z : lv.w)) >> (8 * (q & 3))) & 255u;
-                else if ((int32_t)t == lit + 1) v = (uint32_t)lof & 255u;
-                else if ((int32_t)t == lit + 2) v = ((uint32_t)lof >> 8) & 255u;
-                else v = (uint32_t)(mcode - 15);
-                F.ring[(at + t) & RING_MASK(F)] = (uint8_t)v;
-            }
-        }
-        o.op += total;
-        anchor = lane_val(le, lcnt - 1);
-        lcnt = 0;
-    };
-#endif
     // 4 source bytes at x for the lanes that `need` them: from the window, else memory
     auto seq_at = [&](int32_t x, bool need) -> uint32_t {
         const int32_t ow = x - wb;
@@ -723,9 +651,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             if (K > 1) { LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7) }
 #undef LZ4MI_DUP
             static_assert(kSpecK == 8, "LZ4MI_DUP / LZ4MI_LATER cover distances 1..7");
-#if !LZ4MI_BULK_EMIT
             const uint32_t litv = npend ? load_lit() : 0u;
-#endif
             CPROF(0);
             CPROF_COUNT(8, 1);
             uint32_t tlo = 0, tcd = 0;
@@ -733,19 +659,11 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
                 tlo = T16[h];
                 tcd = gt_code_of(F, h);
             }
-#if LZ4MI_BULK_EMIT
-            if (lcnt > kListMax - kSpecK) {                     // off the chain, while the reads are in flight
-                __builtin_amdgcn_s_setprio(0);
-                emit_list();
-                __builtin_amdgcn_s_setprio(3);
-            }
-#else
             if (npend) {                                        // off the chain, while the reads are in flight
                 __builtin_amdgcn_s_setprio(0);
                 emit_batch(litv);
                 __builtin_amdgcn_s_setprio(3);
             }
-#endif
             // (the read's value is opaque until here: otherwise the compiler consumes it, and
             // waits for it, right after the load, before the emission)
             asm volatile("" : "+v"(tlo) :: "memory");
@@ -791,23 +709,17 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             insert(lane <= J && !later, h, p);
             const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
             const bool hitJ = (__ballot(hit) >> J) & 1ull;
-#if !LZ4MI_BULK_EMIT
             pd_p = p;
             pd_c = cand;
             pd_e = e;
-#endif
             CPROF(3);
             if (hitJ) {
                 CPROF_COUNT(9, 1);
                 int32_t eJ = lane_val(e, J);
                 if ((__ballot(lng) >> J) & 1ull)
                     eJ = pJ + kSpecW + (int32_t)match_extent(j, lane, pJ + kSpecW, cJ + kSpecW, matchlimit - (pJ + kSpecW));
-#if LZ4MI_BULK_EMIT
-                list_add(J + 1, p, cand, lane == J ? eJ : e);
-#else
                 if (lane == J) pd_e = eJ;
                 npend = J + 1;
-#endif
                 S = eJ - pJ;
                 i = eJ;
                 CPROF(4);
@@ -815,12 +727,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             }
             // probe J missed (and inserted itself): the accepted hits go out, the miss chain
             // goes on at the next position
-#if LZ4MI_BULK_EMIT
-            list_add(J, p, cand, e);
-#else
             npend = J;
             if (npend) emit_pending(load_lit());
-#endif
             i = pJ + 1;                                         // (c = 67: step 1)
             c = 68;
             S = 0;
@@ -828,9 +736,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             continue;
         }
         // ================= miss batch: the next 64 probes of the miss chain, starting at i
-#if !LZ4MI_BULK_EMIT
         if (npend) emit_pending(load_lit());
-#endif
         CPROF_COUNT(10, 1);
         const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
         const uint32_t step = (c + lane) >> 6;
@@ -881,15 +787,10 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
         c = 67;
         const int32_t e1 = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
-#if LZ4MI_BULK_EMIT
-        if (lcnt >= kListMax) emit_list();
-        list_add(1, pm, cm, e1);
-#else
         pd_p = pm;
         pd_c = cm;
         pd_e = e1;
         npend = 1;
-#endif
         S = e1 - pm;
         i = e1;
         CPROF(7);
@@ -898,11 +799,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     if (lane == 0)
         for (int k = 0; k < 12; ++k) atomicAdd(&g_cprof[k], (unsigned long long)cprof[k]);
 #endif
-#if LZ4MI_BULK_EMIT
-    if (lcnt) emit_list();
-#else
     if (npend) emit_pending(load_lit());
-#endif
     o = emit_tail(F, o, j, lane, anchor, n - anchor, nullptr);
     ring_flush(F, o, lane);
     for (int64_t t = o.flushed + lane; t < o.op; t += kWave) j.dst[t] = F.ring[t & RING_MASK(F)];

@@ -47,7 +47,7 @@
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
 #ifndef LZ4MI_PER_ALIGN
-#define LZ4MI_PER_ALIGN 0   // 1: long periodic runs stored on the 16-byte grid (A/B switch)
+#define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
 #endif
 #ifndef LZ4MI_ABLATE
