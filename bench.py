@@ -344,7 +344,7 @@ def c_cpu_baseline(batch, threads, target_s=1.5):
                       f"{threads} pthreads, {el:.1f} s wall"}
 
 
-def napi_e2e(batch, nblocks=64):
+def napi_e2e(batch, nblocks=128):
     """LZ4.compress/decompress of the JS drop-in on host buffers (N-API -> liblz4mi), on
     the first `nblocks` generated blocks: PCIe-inclusive, reported beside the bench."""
     import tempfile

@@ -80,24 +80,27 @@ function blockId(bytes) {             // bufferCompress.js:77-82
     return 7;
 }
 
-// Routing (SURVEY.md §8b, DESIGN §5 "Routing"). A batch of b independent blocks costs the GPU
-// about one block's chain latency (every block is one wave, all resident at once) and the host
-// b blocks one after another, so the GPU wins from a block count on that is nearly independent
-// of the block size: the crossovers below are the single-block latencies measured on the box
-// (bench.py `single_block`). A raw-block call is one block: the host's. 'gpu' sends every
-// call to the kernels (tests; the kernels' own parity).
-const HOST_MAX_BLOCKS_COMPRESS = 16;     // tiles216 4 MiB: GPU batch ~45 ms vs host ~3 ms per block
-const HOST_MAX_BLOCKS_DECOMPRESS = 4;    // GPU batch ~5 ms incl. PCIe vs host ~1.2 ms per block
+// Routing (SURVEY.md §8b, DESIGN §5.1). A batch of b independent blocks costs the GPU about
+// one block's chain latency (every block is one wave, all resident at once) plus the PCIe
+// copies, and the host b blocks one after another, so the GPU wins from a block count on that
+// is nearly independent of the block size. The crossovers below are measured on the box
+// (bench.py `single_block` and `napi_end_to_end.crossover`; 4 MiB tiles216: compress GPU
+// ~31 ms for one block vs host 1.1 ms per block, decode GPU ~8-12 ms + 0.09 ms per block vs
+// host 0.23 ms per block). A raw-block call is one block: the host's. 'gpu' / 'host' force
+// one side for every call (tests, and measuring the crossover).
+const HOST_MAX_BLOCKS_COMPRESS = 32;
+const HOST_MAX_BLOCKS_DECOMPRESS = 64;
 let routing = 'auto';
 
-/** 'auto' (default: the measured crossovers above) or 'gpu' (every block call on the GPU). */
+/** 'auto' (default: the measured crossovers above), 'gpu' or 'host' (every block call on that side). */
 export function setRouting(mode) {
-    if (mode !== 'auto' && mode !== 'gpu') throw new TypeError("lz4mi: routing must be 'auto' or 'gpu'");
+    if (mode !== 'auto' && mode !== 'gpu' && mode !== 'host')
+        throw new TypeError("lz4mi: routing must be 'auto', 'gpu' or 'host'");
     routing = mode;
 }
 
 const hostRoute = (nblocks, max) => {
-    if (routing !== 'auto' || nblocks > max) return false;
+    if (routing === 'gpu' || (routing === 'auto' && nblocks > max)) return false;
     requireDevice();
     return true;
 };
@@ -242,8 +245,7 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
         if (dictLen > 0 && pos < end) {
             const n = Math.min(bsize, end - pos);
             const scratch = new Uint8Array(n + ((n / 255) | 0) + 16);
-            requireDevice();
-            const c = native.compressBlockHost(work, scratch, pos, n, table, 0);     // one chain: host route
+            const c = compressRaw(work, scratch, pos, n, table, 0);     // one chain: the host's unless 'gpu'
             emit(pos, n, c, scratch.subarray(0, Math.max(0, Math.min(c, scratch.length))));
             table.fill(0);
             pos += n;
@@ -387,8 +389,7 @@ export function decompress(input, dictionary = null, verifyChecksum = true, veri
     const independent = (flg & 0x20) !== 0;
     let ncomp = 0;
     for (const b of blocks) if (!b.raw) ncomp++;
-    const host = routing === 'auto' && (!independent || ncomp <= HOST_MAX_BLOCKS_DECOMPRESS);
-    if (host) requireDevice();
+    const host = hostRoute(independent ? ncomp : 0, HOST_MAX_BLOCKS_DECOMPRESS);
     const decodeBlock = host ? native.decompressBlockHost : native.decompressBlock;
     let result;
     if (expected > 0) {

@@ -4,24 +4,28 @@
 // Prints one JSON line: LZ4.compress with independent blocks (batched), LZ4.compress
 // with the reference's default dependent blocks (the layer's host route: one serial chain,
 // the table carried; checked to decode back), LZ4.decompress in 'spec' and 'reference'
-// (default) modes, and the decode of the dependent frame.
+// (default) modes, the decode of the dependent frame, all under the default routing; then
+// the routing crossover: independent-block compress / decompress (spec) of the first b
+// blocks with every call forced to the GPU and to the host codec (DESIGN §5.1).
 import fs from 'fs';
 import { LZ4 } from '../divortio-lz4_amd/js/lz4mi.mjs';
 
 const input = new Uint8Array(fs.readFileSync(process.argv[2]));
 const reps = Number(process.argv[3] || 3);
 const depBytes = Math.min(input.length, Number(process.argv[4] || (16 << 20)));
+const BS = 4194304;
 const now = () => Number(process.hrtime.bigint()) / 1e9;
-const rate = (bytes, fn, n) => {
+const secs = (fn, n) => {
     fn();                                 // warm-up
     const t0 = now();
     for (let r = 0; r < n; r++) fn();
-    return +(bytes * n / (now() - t0) / 1e9).toFixed(3);
+    return (now() - t0) / n;
 };
-const out = { bytes: input.length };
-let frame = LZ4.compress(input, null, 4194304, true, false);
+const rate = (bytes, fn, n) => +(bytes / secs(fn, n) / 1e9).toFixed(3);
+const out = { bytes: input.length, routing: 'auto' };
+let frame = LZ4.compress(input, null, BS, true, false);
 out.ratio = +(input.length / frame.length).toFixed(3);
-out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, 4194304, true, false); }, reps);
+out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, BS, true, false); }, reps);
 const dep = input.subarray(0, depBytes);
 let depFrame = null;
 out.compress_dependent_default_GBps = rate(dep.length, () => { depFrame = LZ4.compress(dep); }, 1);
@@ -38,6 +42,21 @@ for (const mode of ['spec', 'reference']) {
         throw new Error(`${mode} round trip mismatch`);
     out[`decompress_${mode}_GBps`] = rate(input.length, () => LZ4.decompress(frame), reps);
 }
+LZ4.setDecodeMode('spec');
+const cross = { block_bytes: BS, blocks: [], compress_ms: { gpu: [], host: [] }, decompress_ms: { gpu: [], host: [] } };
+for (const b of [1, 4, 16, 32, 64, 128]) {
+    if (b * BS > input.length) break;
+    const sub = input.subarray(0, b * BS);
+    cross.blocks.push(b);
+    for (const side of ['gpu', 'host']) {
+        LZ4.setRouting(side);
+        let f = null;
+        cross.compress_ms[side].push(+(secs(() => { f = LZ4.compress(sub, null, BS, true, false); }, 2) * 1e3).toFixed(2));
+        cross.decompress_ms[side].push(+(secs(() => LZ4.decompress(f), 2) * 1e3).toFixed(2));
+    }
+}
+LZ4.setRouting('auto');
 LZ4.setDecodeMode('reference');
+out.crossover = cross;
 out.note = 'host buffers through N-API (PCIe-inclusive): not the device-resident bench value';
 console.log(JSON.stringify(out));
