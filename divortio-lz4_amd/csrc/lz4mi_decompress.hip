@@ -1513,6 +1513,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         wait_vmem();
         settle(pf0);    // (so the next chunk's stage does not wait for this chunk's stores)
         settle(pf1);
+        PROF(21);
         // output -> sequence map for remap_src, in the (now idle) next-token table
         uint32_t msh = 4;
         while ((total >> msh) >= kLim) ++msh;
@@ -1522,6 +1523,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             for (uint32_t b = (t0 + (1u << msh) - 1) >> msh; (b << msh) < t1; ++b) S.nxt[b] = (uint16_t)k;
         }
         __syncthreads();
+        PROF(22);
         uint32_t pend = 0;    // bit i: the match of sequence 64i+lane is still to be written
         uint32_t ready = 0;   // bit i: ... is written by this lane in this round
         uint32_t rbits = 0;   // bit i: ... reads a remapped source (SeqInfo::rsrc)
@@ -1537,6 +1539,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 lane_literals(c, S, longL ? no_run() : L);
                 for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
             }
+            PROF(23);
             if (k < nseq) {
                 const int32_t t0 = q.out;
                 M = match_run(c, t0 + q.ll, q.off, q.ml);

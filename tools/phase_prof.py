@@ -54,7 +54,8 @@ def main():
                   f"rounds/chunk={v[11] / n / max(1, chunks):.2f} cuts/block={v[12] / n:.1f} ok={ok}")
             print("   us/chunk:", per, flush=True)
             extra = {nm: round(v[i] / 100.0 / n / max(1, chunks), 3) for i, nm in
-                     ((16, "r1_groupsetup"), (17, "r1_literals"), (18, "r1_slow+long"), (19, "r1_pipe"), (20, "rN_compact+wait"))}
+                     ((21, "r1_wait"), (22, "r1_map"), (23, "r1_litruns"), (16, "r1_remap"), (17, "r1_split_lits"),
+                      (18, "r1_slow+long"), (19, "r1_pipe"), (20, "rN_compact+wait"))}
             print("   round-1 split:", extra)
             print(f"   cert iterations/chunk={v[13] / n / max(1, chunks):.2f} initially-bad lanes/chunk="
                   f"{v[14] / n / max(1, chunks):.2f} warm-up steps/lane/chunk={v[15] / n / max(1, chunks):.2f}")
