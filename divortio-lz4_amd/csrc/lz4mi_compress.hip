@@ -64,6 +64,9 @@ __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
 }
 
+#ifndef LZ4MI_EMIT_LANES
+#define LZ4MI_EMIT_LANES 1   // a batch's sequences written by their own lanes (4 byte stores); 0: one lane per output byte
+#endif
 #ifndef LZ4MI_SHFL_READLANE
 #define LZ4MI_SHFL_READLANE 0   // 1: the two per-batch lane gathers as v_readlane (measured slower: SGPR spills)
 #endif
@@ -560,6 +563,26 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         incl += dpp<kRowShr4>(0u, incl);
         const uint32_t start = incl - size;
         const int32_t total = (int32_t)lane_val(incl, npend - 1);
+#if LZ4MI_EMIT_LANES
+        // each sequence's lane writes its token, offset and length byte; lanes 1 .. lit0 the
+        // literal bytes of sequence 0 (which starts the batch)
+        ring_reserve(F, o, lane, total);
+        {
+            const uint32_t base = (uint32_t)o.op, msk = (uint32_t)RING_MASK(F);
+            const uint32_t off = (uint32_t)(pd_p - pd_c);
+            if (mine) {
+                const uint32_t a = base + start, b = a + 1u + (uint32_t)lit;
+                F.ring[a & msk] = (uint8_t)(((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode));
+                F.ring[b & msk] = (uint8_t)off;
+                F.ring[(b + 1u) & msk] = (uint8_t)(off >> 8);
+                if (mcode >= 15) F.ring[(b + 2u) & msk] = (uint8_t)(mcode - 15);
+            }
+            if (lane >= 1 && lane <= lit0) F.ring[(base + (uint32_t)lane) & msk] = (uint8_t)litv;
+        }
+        o.op += total;
+        anchor = lane_val(pd_e, npend - 1);
+        npend = 0;
+#else
         const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
         const uint32_t off = (uint32_t)(pd_p - pd_c);
         ring_reserve(F, o, lane, total);
@@ -587,6 +610,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         o.op += total;
         anchor = lane_val(pd_e, npend - 1);
         npend = 0;
+#endif
     };
     auto insert = [&](bool ins, uint32_t h, int32_t p) {   // distinct hashes among inserting lanes
         if (ins) {

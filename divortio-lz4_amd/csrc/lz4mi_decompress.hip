@@ -1515,7 +1515,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         settle(pf1);
         PROF(21);
         // output -> sequence map for remap_src, in the (now idle) next-token table
-        uint32_t msh = 4;
+        uint32_t msh = 5;   // output -> sequence map granule: 32 bytes (16: +1.8 % on tiles216)
         while ((total >> msh) >= kLim) ++msh;
         for (uint32_t k = lane; k < nseq; k += kWave) {
             const uint32_t t0 = S.t_seq[k].x - (uint32_t)c.O;
