@@ -417,6 +417,56 @@ __device__ __forceinline__ void emit_seq(SH& F, FastOut& o, const CompJob& j, in
 }
 
 
+// A batch's common-case sequences into the ring (lanes k < npend: sequence k at ring offset
+// start, `total` bytes in all; sequence 0 alone has literals, lit0 < 15, whose byte l - 1 lane
+// l holds in litv; every match length field at most one extra byte).
+template <class SH>
+__device__ __forceinline__ void ring_seqs(SH& F, FastOut& o, int lane, int npend, int32_t lit0, int32_t mcode,
+                                          uint32_t off, uint32_t start, int32_t total, uint32_t litv) {
+    const bool mine = lane < npend;
+    const int32_t lit = lane == 0 ? lit0 : 0;
+    ring_reserve(F, o, lane, total);
+#if LZ4MI_EMIT_LANES
+    // each sequence's own lane writes its token, offset and length byte; lanes 1 .. lit0 the
+    // literal bytes of sequence 0 (which starts the batch)
+    const uint32_t base = (uint32_t)o.op, msk = (uint32_t)RING_MASK(F);
+    if (mine) {
+        const uint32_t a = base + start, b = a + 1u + (uint32_t)lit;
+        F.ring[a & msk] = (uint8_t)(((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode));
+        F.ring[b & msk] = (uint8_t)off;
+        F.ring[(b + 1u) & msk] = (uint8_t)(off >> 8);
+        if (mcode >= 15) F.ring[(b + 2u) & msk] = (uint8_t)(mcode - 15);
+    }
+    if (lane >= 1 && lane <= lit0) F.ring[(base + (uint32_t)lane) & msk] = (uint8_t)litv;
+#else
+    // output lane t finds its sequence among the <= 8 starts and writes byte t
+    const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
+    int32_t r = lane, cl = 0;
+    uint32_t ct = 0, co = 0, cm = 0;
+    for (int k = 0; k < npend; ++k) {
+        const int32_t sk = (int32_t)lane_val(start, k);
+        if (lane >= sk) {
+            r = lane - sk;
+            cl = k == 0 ? lit0 : 0;
+            ct = lane_val(tok, k);
+            co = lane_val(off, k);
+            cm = (uint32_t)lane_val(mcode, k);
+        }
+    }
+    if (lane < total) {
+        uint32_t v;
+        if (r == 0) v = ct;
+        else if (r <= cl) v = litv;
+        else if (r == cl + 1) v = co & 255;
+        else if (r == cl + 2) v = (co >> 8) & 255;
+        else v = cm - 15;
+        F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
+    }
+#endif
+    o.op += total;
+}
+
+
 // ---------------------------------------------------------------------------
 // Batch encoder tables: one per block in global scratch, each entry the probed
 // position's low 15 bits (32 KiB per block) plus a 2-bit code of its 32 KiB epoch in
@@ -563,54 +613,9 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         incl += dpp<kRowShr4>(0u, incl);
         const uint32_t start = incl - size;
         const int32_t total = (int32_t)lane_val(incl, npend - 1);
-#if LZ4MI_EMIT_LANES
-        // each sequence's lane writes its token, offset and length byte; lanes 1 .. lit0 the
-        // literal bytes of sequence 0 (which starts the batch)
-        ring_reserve(F, o, lane, total);
-        {
-            const uint32_t base = (uint32_t)o.op, msk = (uint32_t)RING_MASK(F);
-            const uint32_t off = (uint32_t)(pd_p - pd_c);
-            if (mine) {
-                const uint32_t a = base + start, b = a + 1u + (uint32_t)lit;
-                F.ring[a & msk] = (uint8_t)(((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode));
-                F.ring[b & msk] = (uint8_t)off;
-                F.ring[(b + 1u) & msk] = (uint8_t)(off >> 8);
-                if (mcode >= 15) F.ring[(b + 2u) & msk] = (uint8_t)(mcode - 15);
-            }
-            if (lane >= 1 && lane <= lit0) F.ring[(base + (uint32_t)lane) & msk] = (uint8_t)litv;
-        }
-        o.op += total;
+        ring_seqs(F, o, lane, npend, lit0, mcode, (uint32_t)(pd_p - pd_c), start, total, litv);
         anchor = lane_val(pd_e, npend - 1);
         npend = 0;
-#else
-        const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
-        const uint32_t off = (uint32_t)(pd_p - pd_c);
-        ring_reserve(F, o, lane, total);
-        int32_t r = lane, cl = 0;
-        uint32_t ct = 0, co = 0, cm = 0;
-        for (int k = 0; k < npend; ++k) {
-            const int32_t sk = (int32_t)lane_val(start, k);
-            if (lane >= sk) {
-                r = lane - sk;
-                cl = k == 0 ? lit0 : 0;
-                ct = lane_val(tok, k);
-                co = lane_val(off, k);
-                cm = (uint32_t)lane_val(mcode, k);
-            }
-        }
-        if (lane < total) {
-            uint32_t v;
-            if (r == 0) v = ct;
-            else if (r <= cl) v = litv;                         // sequence 0 starts at 0: lane r holds byte r - 1
-            else if (r == cl + 1) v = co & 255;
-            else if (r == cl + 2) v = (co >> 8) & 255;
-            else v = cm - 15;
-            F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
-        }
-        o.op += total;
-        anchor = lane_val(pd_e, npend - 1);
-        npend = 0;
-#endif
     };
     auto insert = [&](bool ins, uint32_t h, int32_t p) {   // distinct hashes among inserting lanes
         if (ins) {
@@ -950,31 +955,7 @@ __device__ int64_t compress_block_chain2(const CompJob& j, ChainShared& F, int l
         incl += dpp<kRowShr4>(0u, incl);
         const uint32_t st = incl - size;
         const int32_t total = (int32_t)lane_val(incl, npend - 1);
-        const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
-        const uint32_t off = (uint32_t)(pd_p - pd_c);
-        ring_reserve(F, o, lane, total);
-        int32_t rr = lane, cl = 0;
-        uint32_t ct = 0, co = 0, cm = 0;
-        for (int k = 0; k < npend; ++k) {
-            const int32_t sk = (int32_t)lane_val(st, k);
-            if (lane >= sk) {
-                rr = lane - sk;
-                cl = k == 0 ? lit0 : 0;
-                ct = lane_val(tok, k);
-                co = lane_val(off, k);
-                cm = (uint32_t)lane_val(mcode, k);
-            }
-        }
-        if (lane < total) {
-            uint32_t v;
-            if (rr == 0) v = ct;
-            else if (rr <= cl) v = litv;
-            else if (rr == cl + 1) v = co & 255;
-            else if (rr == cl + 2) v = (co >> 8) & 255;
-            else v = cm - 15;
-            F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
-        }
-        o.op += total;
+        ring_seqs(F, o, lane, npend, lit0, mcode, (uint32_t)(pd_p - pd_c), st, total, litv);
         anchor = lane_val(pd_e, npend - 1);
         npend = 0;
     };
