@@ -46,6 +46,9 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#ifndef LZ4MI_LIT_LATE
+#define LZ4MI_LIT_LATE 0   // 1: round 1's literal runs written after its match copies (A/B switch)
+#endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
@@ -1535,12 +1538,14 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             Run M = no_run(), ML = no_run();
             SeqInfo q = seq_info(S, k < nseq ? k : 0u);
             if (k >= nseq) q.ll = 0;
+#if !LZ4MI_LIT_LATE
             {   // the literal runs first (their registers are free before the remap)
                 const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
                 const bool longL = L.n > kLaneBytes;
                 lane_literals(c, S, longL ? no_run() : L);
                 for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
             }
+#endif
             PROF(23);
             if (k < nseq) {
                 const int32_t t0 = q.out;
@@ -1589,6 +1594,19 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #if LZ4MI_PIECES
         piece_pipe(c, S, ready, rbits, lane, nseq, dfr, LZ4MI_DEFER && !cut && !a.f1check && __ballot(pend != 0) == 0,
                    nlit_pack);
+#if LZ4MI_LIT_LATE
+        // the literal runs after round 1's match copies (nothing in round 1 reads this chunk's
+        // output from memory; the next round's opening wait covers these stores)
+        for (uint32_t i = 0; 64 * i < nseq; ++i) {
+            const uint32_t k = 64 * i + lane;
+            SeqInfo q = seq_info(S, k < nseq ? k : 0u);
+            if (k >= nseq) q.ll = 0;
+            const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
+            const bool longL = L.n > kLaneBytes;
+            lane_literals(c, S, longL ? no_run() : L);
+            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
+        }
+#endif
         if (dfr.any) goto chunk_done;   // nothing else to write (and the deferred batch stays out of
                                         // the rounds' registers)
 #else

@@ -96,7 +96,7 @@ def main():
     for gen in args.gens.split(","):
         raw = make_raw(torch, lz4mi, gen, n, sp)
         slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
-        comp = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+        comp = torch.zeros(n * slot, dtype=torch.uint8, device="cuda")
         roff = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
         rlen = torch.full((n,), BLOCK, dtype=torch.int32, device="cuda")
         coff = torch.arange(n, dtype=torch.int64, device="cuda") * slot
@@ -119,6 +119,9 @@ def main():
                     r = L.lz4mi_compress_blocks(raw.data_ptr(), roff.data_ptr(), rlen.data_ptr(), comp.data_ptr(),
                                                 coff.data_ptr(), clen.data_ptr(), n, 1, sp)
                 assert r == 0
+            dec.zero_()      # (so "ok" is this build's output, not a leftover of the previous one)
+            comp.zero_() if args.what != "decompress" else None
+            torch.cuda.synchronize()
             run()
             torch.cuda.synchronize()
             times = []
