@@ -64,17 +64,6 @@ __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
 }
 
-#ifndef LZ4MI_MSKOR
-#define LZ4MI_MSKOR 1   // epoch-code inserts as one ds_mskor_b32 (0: an LDS atomic AND + OR)
-#endif
-// One atomic LDS read-modify-write: *p = (*p & ~clear) | set (ds_mskor_b32; LDS operations of
-// a wave execute in order, so later LDS reads of *p see it).
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ void lds_mskor(uint32_t* p, uint32_t clear, uint32_t set) {
-    const uint32_t a = (uint32_t)(uintptr_t)(lds_u32*)p;
-    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(clear), "v"(set) : "memory");
-}
-
 #ifndef LZ4MI_EMIT_LANES
 #define LZ4MI_EMIT_LANES 1   // a batch's sequences written by their own lanes (4 byte stores); 0: one lane per output byte
 #endif
@@ -632,12 +621,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         if (ins) {
             T16[h] = (uint16_t)(p & 0x7FFF);
             const uint32_t sh = (h & 15) * 2;                  // two hashes may share a code word: LDS atomics
-#if LZ4MI_MSKOR
-            lds_mskor(&F.code[h >> 4], 3u << sh, (uint32_t)(g & 3) << sh);
-#else
             atomicAnd(&F.code[h >> 4], ~(3u << sh));
             atomicOr(&F.code[h >> 4], (uint32_t)(g & 3) << sh);
-#endif
         }
     };
     // 4 source bytes at x for the lanes that `need` them: from the window, else memory

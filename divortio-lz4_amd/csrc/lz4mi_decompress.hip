@@ -46,6 +46,9 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#ifndef LZ4MI_LIT16
+#define LZ4MI_LIT16 1   // short literal runs followed by their match as one 16-byte store (A/B switch)
+#endif
 #ifndef LZ4MI_LIT_LATE
 #define LZ4MI_LIT_LATE 0   // 1: round 1's literal runs written after its match copies (A/B switch)
 #endif
@@ -1036,7 +1039,10 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
 }
 
 // Each lane copies its own short literal runs (LDS -> output; no vector-memory loads).
-__device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L) {
+// `tail`: bytes after the run that this wave writes later in program order (the sequence's
+// match): a run shorter than 16 bytes with n + tail >= 16 goes out as one 16-byte store whose
+// last bytes the match overwrites (a wave's stores complete in issue order).
+__device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L, int32_t tail = 0) {
     const int32_t n = L.kind == R_NONE ? 0 : L.n;
     const int np = n >= 16 ? (n + 15) >> 4 : 0;
     for (int q = 0; __ballot(q < np) != 0; q += 2) {       // runs of >= 16 bytes: 16-byte pieces
@@ -1048,7 +1054,9 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         if (q + 1 < np) out16(c.dst + L.y + d1, v1);
     }
     if (__ballot(n > 0 && n < 16)) {                       // shorter runs: 8/4/2/1-byte pieces by the bits of n
-        if (n > 0 && n < 16) {                             // (one stage read, no per-width branches)
+        if (LZ4MI_LIT16 && n > 0 && n < 16 && n + tail >= 16) {
+            if (LZ4MI_ABLATE != 4) out16(c.dst + L.y, stage16(S.stage, L.src));
+        } else if (n > 0 && n < 16) {                      // (one stage read, no per-width branches)
             const uint4 v = stage16(S.stage, L.src);
             uint8_t* d = c.dst + L.y;
             uint64_t lo = v.x | ((uint64_t)v.y << 32);
@@ -1542,7 +1550,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             {   // the literal runs first (their registers are free before the remap)
                 const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
                 const bool longL = L.n > kLaneBytes;
-                lane_literals(c, S, longL ? no_run() : L);
+                const int32_t ms = q.out + q.ll;
+                lane_literals(c, S, longL ? no_run() : L, k < nseq ? min((int32_t)q.ml, (int32_t)c.cap - ms) : 0);
                 for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
             }
 #endif
@@ -1584,7 +1593,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
             PROF(16);
-            lane_literals(c, S, longML ? no_run() : ML);
+            lane_literals(c, S, longML ? no_run() : ML, M.kind != R_NONE ? M.n : 0);
             PROF(17);
             for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)), no_pat());
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
