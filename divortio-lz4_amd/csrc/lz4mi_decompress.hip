@@ -46,6 +46,9 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#ifndef LZ4MI_LIT_OVERLAP
+#define LZ4MI_LIT_OVERLAP 1   // short literal runs read before the remap, written after it (A/B switch)
+#endif
 #ifndef LZ4MI_LIT16
 #define LZ4MI_LIT16 1   // short literal runs followed by their match as one 16-byte store (A/B switch)
 #endif
@@ -1038,6 +1041,25 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
     else pipe<R_HIST, false, kWaveB>(c, S, g);
 }
 
+// A literal run of 1..15 bytes (v: its stage bytes): one 16-byte store when the bytes after it
+// are this wave's to overwrite later (`tail`, see lane_literals), else 8/4/2/1-byte pieces by
+// the bits of n (no per-width branches).
+__device__ __forceinline__ void short_literals(const Ctx& c, int32_t y, int32_t n, const uint4& v, int32_t tail) {
+    if (LZ4MI_ABLATE == 4) return;
+    if (LZ4MI_LIT16 && n + tail >= 16) {
+        out16(c.dst + y, v);
+        return;
+    }
+    uint8_t* d = c.dst + y;
+    uint64_t lo = v.x | ((uint64_t)v.y << 32);
+    const uint64_t hi = v.z | ((uint64_t)v.w << 32);
+    int32_t o = 0;
+    if (n & 8) { __builtin_memcpy(d, &lo, 8); lo = hi; o = 8; }
+    if (n & 4) { const uint32_t t = (uint32_t)lo; __builtin_memcpy(d + o, &t, 4); lo >>= 32; o += 4; }
+    if (n & 2) { const uint16_t t = (uint16_t)lo; __builtin_memcpy(d + o, &t, 2); lo >>= 16; o += 2; }
+    if (n & 1) d[o] = (uint8_t)lo;
+}
+
 // Each lane copies its own short literal runs (LDS -> output; no vector-memory loads).
 // `tail`: bytes after the run that this wave writes later in program order (the sequence's
 // match): a run shorter than 16 bytes with n + tail >= 16 goes out as one 16-byte store whose
@@ -1053,22 +1075,8 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         if (q < np) out16(c.dst + L.y + d0, v0);
         if (q + 1 < np) out16(c.dst + L.y + d1, v1);
     }
-    if (__ballot(n > 0 && n < 16)) {                       // shorter runs: 8/4/2/1-byte pieces by the bits of n
-        if (LZ4MI_LIT16 && n > 0 && n < 16 && n + tail >= 16) {
-            if (LZ4MI_ABLATE != 4) out16(c.dst + L.y, stage16(S.stage, L.src));
-        } else if (n > 0 && n < 16) {                      // (one stage read, no per-width branches)
-            const uint4 v = stage16(S.stage, L.src);
-            uint8_t* d = c.dst + L.y;
-            uint64_t lo = v.x | ((uint64_t)v.y << 32);
-            const uint64_t hi = v.z | ((uint64_t)v.w << 32);
-            int32_t o = 0;
-            if (LZ4MI_ABLATE != 4) {
-                if (n & 8) { __builtin_memcpy(d, &lo, 8); lo = hi; o = 8; }
-                if (n & 4) { const uint32_t t = (uint32_t)lo; __builtin_memcpy(d + o, &t, 4); lo >>= 32; o += 4; }
-                if (n & 2) { const uint16_t t = (uint16_t)lo; __builtin_memcpy(d + o, &t, 2); lo >>= 16; o += 2; }
-                if (n & 1) d[o] = (uint8_t)lo;
-            }
-        }
+    if (__ballot(n > 0 && n < 16)) {                       // shorter runs: one stage read
+        if (n > 0 && n < 16) short_literals(c, L.y, n, stage16(S.stage, L.src), tail);
     }
 }
 
@@ -1546,7 +1554,20 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             Run M = no_run(), ML = no_run();
             SeqInfo q = seq_info(S, k < nseq ? k : 0u);
             if (k >= nseq) q.ll = 0;
-#if !LZ4MI_LIT_LATE
+#if LZ4MI_LIT_OVERLAP
+            // a literal run under 16 bytes (the usual one): its stage bytes are read here and
+            // written after the remap, so this LDS round trip overlaps the remap's
+            const bool shortL = q.ll > 0 && q.ll < 16;
+            const int32_t ltail = k < nseq ? min((int32_t)q.ml, (int32_t)c.cap - (int32_t)(q.out + q.ll)) : 0;
+            uint4 lv = make_uint4(0, 0, 0, 0);
+            if (shortL) lv = stage16(S.stage, q.lit);
+            {   // longer runs now
+                const Run L = q.ll >= 16 ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
+                const bool longL = L.n > kLaneBytes;
+                lane_literals(c, S, longL ? no_run() : L);
+                for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
+            }
+#elif !LZ4MI_LIT_LATE
             {   // the literal runs first (their registers are free before the remap)
                 const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
                 const bool longL = L.n > kLaneBytes;
@@ -1588,6 +1609,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     }
                 }
             }
+#if LZ4MI_LIT_OVERLAP
+            if (shortL) short_literals(c, q.out, q.ll, lv, ltail);
+#endif
             const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
             const bool longML = ML.n > kLaneBytes;
             const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
