@@ -46,15 +46,6 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
-#ifndef LZ4MI_LIT_OVERLAP
-#define LZ4MI_LIT_OVERLAP 1   // short literal runs read before the remap, written after it (A/B switch)
-#endif
-#ifndef LZ4MI_LIT16
-#define LZ4MI_LIT16 1   // short literal runs followed by their match as one 16-byte store (A/B switch)
-#endif
-#ifndef LZ4MI_LIT_LATE
-#define LZ4MI_LIT_LATE 0   // 1: round 1's literal runs written after its match copies (A/B switch)
-#endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
@@ -1041,15 +1032,10 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
     else pipe<R_HIST, false, kWaveB>(c, S, g);
 }
 
-// A literal run of 1..15 bytes (v: its stage bytes): one 16-byte store when the bytes after it
-// are this wave's to overwrite later (`tail`, see lane_literals), else 8/4/2/1-byte pieces by
-// the bits of n (no per-width branches).
-__device__ __forceinline__ void short_literals(const Ctx& c, int32_t y, int32_t n, const uint4& v, int32_t tail) {
+// A literal run of 1..15 bytes (v: its stage bytes) in 8/4/2/1-byte pieces by the bits of n
+// (no per-width branches).
+__device__ __forceinline__ void short_literals(const Ctx& c, int32_t y, int32_t n, const uint4& v) {
     if (LZ4MI_ABLATE == 4) return;
-    if (LZ4MI_LIT16 && n + tail >= 16) {
-        out16(c.dst + y, v);
-        return;
-    }
     uint8_t* d = c.dst + y;
     uint64_t lo = v.x | ((uint64_t)v.y << 32);
     const uint64_t hi = v.z | ((uint64_t)v.w << 32);
@@ -1061,10 +1047,7 @@ __device__ __forceinline__ void short_literals(const Ctx& c, int32_t y, int32_t 
 }
 
 // Each lane copies its own short literal runs (LDS -> output; no vector-memory loads).
-// `tail`: bytes after the run that this wave writes later in program order (the sequence's
-// match): a run shorter than 16 bytes with n + tail >= 16 goes out as one 16-byte store whose
-// last bytes the match overwrites (a wave's stores complete in issue order).
-__device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L, int32_t tail = 0) {
+__device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, const Run& L) {
     const int32_t n = L.kind == R_NONE ? 0 : L.n;
     const int np = n >= 16 ? (n + 15) >> 4 : 0;
     for (int q = 0; __ballot(q < np) != 0; q += 2) {       // runs of >= 16 bytes: 16-byte pieces
@@ -1076,7 +1059,7 @@ __device__ __forceinline__ void lane_literals(const Ctx& c, const DecShared& S, 
         if (q + 1 < np) out16(c.dst + L.y + d1, v1);
     }
     if (__ballot(n > 0 && n < 16)) {                       // shorter runs: one stage read
-        if (n > 0 && n < 16) short_literals(c, L.y, n, stage16(S.stage, L.src), tail);
+        if (n > 0 && n < 16) short_literals(c, L.y, n, stage16(S.stage, L.src));
     }
 }
 
@@ -1554,28 +1537,12 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             Run M = no_run(), ML = no_run();
             SeqInfo q = seq_info(S, k < nseq ? k : 0u);
             if (k >= nseq) q.ll = 0;
-#if LZ4MI_LIT_OVERLAP
-            // a literal run under 16 bytes (the usual one): its stage bytes are read here and
-            // written after the remap, so this LDS round trip overlaps the remap's
-            const bool shortL = q.ll > 0 && q.ll < 16;
-            const int32_t ltail = k < nseq ? min((int32_t)q.ml, (int32_t)c.cap - (int32_t)(q.out + q.ll)) : 0;
-            uint4 lv = make_uint4(0, 0, 0, 0);
-            if (shortL) lv = stage16(S.stage, q.lit);
-            {   // longer runs now
-                const Run L = q.ll >= 16 ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
+            {   // the literal runs first (their registers are free before the remap)
+                const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
                 const bool longL = L.n > kLaneBytes;
                 lane_literals(c, S, longL ? no_run() : L);
                 for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
             }
-#elif !LZ4MI_LIT_LATE
-            {   // the literal runs first (their registers are free before the remap)
-                const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
-                const bool longL = L.n > kLaneBytes;
-                const int32_t ms = q.out + q.ll;
-                lane_literals(c, S, longL ? no_run() : L, k < nseq ? min((int32_t)q.ml, (int32_t)c.cap - ms) : 0);
-                for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
-            }
-#endif
             PROF(23);
             if (k < nseq) {
                 const int32_t t0 = q.out;
@@ -1609,15 +1576,12 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     }
                 }
             }
-#if LZ4MI_LIT_OVERLAP
-            if (shortL) short_literals(c, q.out, q.ll, lv, ltail);
-#endif
             const bool longM = M.kind != R_NONE && M.n > kLaneBytes;
             const bool longML = ML.n > kLaneBytes;
             const bool fastM = M.kind == R_HIST && M.period == 0 && M.n >= 16;
             if (M.kind != R_NONE && !longM && fastM) ready |= 1u << i;
             PROF(16);
-            lane_literals(c, S, longML ? no_run() : ML, M.kind != R_NONE ? M.n : 0);
+            lane_literals(c, S, longML ? no_run() : ML);
             PROF(17);
             for (uint64_t lm = __ballot(longML); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(ML, __builtin_ctzll(lm)), no_pat());
             if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
@@ -1627,19 +1591,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #if LZ4MI_PIECES
         piece_pipe(c, S, ready, rbits, lane, nseq, dfr, LZ4MI_DEFER && !cut && !a.f1check && __ballot(pend != 0) == 0,
                    nlit_pack);
-#if LZ4MI_LIT_LATE
-        // the literal runs after round 1's match copies (nothing in round 1 reads this chunk's
-        // output from memory; the next round's opening wait covers these stores)
-        for (uint32_t i = 0; 64 * i < nseq; ++i) {
-            const uint32_t k = 64 * i + lane;
-            SeqInfo q = seq_info(S, k < nseq ? k : 0u);
-            if (k >= nseq) q.ll = 0;
-            const Run L = q.ll ? Run{q.out, q.ll, q.lit, 0, R_LDS} : no_run();
-            const bool longL = L.n > kLaneBytes;
-            lane_literals(c, S, longL ? no_run() : L);
-            for (uint64_t lm = __ballot(longL); lm; lm &= lm - 1) wave_run(c, S, lane, shfl_run(L, __builtin_ctzll(lm)), no_pat());
-        }
-#endif
         if (dfr.any) goto chunk_done;   // nothing else to write (and the deferred batch stays out of
                                         // the rounds' registers)
 #else
