@@ -659,8 +659,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             int K;
             {
                 const int32_t lim = min(mflimit - 1, ((g + 1) << 15) - 1) - i;   // same epoch, before mflimit
-                K = 1 + lim / S;
-                if (K > kmax) K = kmax;
+                // (a division only near an epoch or block end: it is ~30 instructions on the chain)
+                K = lim >= (kmax - 1) * S ? kmax : 1 + lim / S;
             }
             const bool act = lane < K;
             const int32_t p = i + lane * S;
