@@ -528,6 +528,33 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
     return make_uint4(ld_u32(j, p), ld_u32(j, p + 4), ld_u32(j, p + 8), ld_u32(j, p + 12));
 }
 
+#ifndef LZ4MI_OFF32
+#define LZ4MI_OFF32 1   // batch encoder loads as 32-bit offsets from the block's base (A/B switch)
+#endif
+// The batch encoder's loads (blocks < 2^31 bytes, lim = the block's length): 32-bit bounds
+// tests and a 32-bit unsigned offset from the block's (scalar) base, so the load takes the
+// scalar-base form instead of a 64-bit per-lane address. Zero outside [0, lim).
+__device__ __forceinline__ uint4 ld16o(const CompJob& j, uint32_t lim, int32_t p) {
+#if LZ4MI_OFF32
+    if ((uint32_t)p < lim && lim - (uint32_t)p >= 16u) {
+        uint4 v;
+        __builtin_memcpy(&v, j.src + (uint32_t)p, 16);
+        return v;
+    }
+#endif
+    return ld16(j, p);
+}
+__device__ __forceinline__ uint32_t ld_u32o(const CompJob& j, uint32_t lim, int32_t p) {
+#if LZ4MI_OFF32
+    if ((uint32_t)p < lim && lim - (uint32_t)p >= 4u) {
+        uint32_t v;
+        __builtin_memcpy(&v, j.src + (uint32_t)p, 4);
+        return v;
+    }
+#endif
+    return ld_u32(j, p);
+}
+
 // Index of the first nonzero byte of x (16 if none).
 __device__ __forceinline__ uint32_t first_nz16(uint4 x) {
     return x.x ? (__builtin_ctz(x.x) >> 3)
@@ -546,6 +573,7 @@ struct GtsShared {
 
 __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T, int lane) {
     const int32_t n = j.len;
+    const uint32_t n32 = (uint32_t)j.src_total;   // (= n: the block is the whole source)
     const int32_t mflimit = n - 12, matchlimit = n - 5;
     FastOut o{j.dst, 0, 0};
     int32_t i = 0, anchor = 0;
@@ -632,7 +660,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         uint32_t v = 0;
         if (need && inw) v = funnel(F.win[ow >> 2], F.win[(ow >> 2) + 1], (uint32_t)(ow & 3));
         if (__ballot(need && !inw)) {   // (waited for here, not where the paths join: that wait would
-            if (need && !inw) v = ld_u32(j, x);   // also cover the previous batch's table stores)
+            if (need && !inw) v = ld_u32o(j, n32, x);   // also cover the previous batch's table stores)
             wait_vmem();
         }
         settle32(v);
@@ -641,8 +669,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     // window refill at base b: loads issued now (with a round trip's other loads), written after its wait
     uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
     auto refill_issue = [&](int32_t b) {
-        r0 = ld16(j, (int64_t)b + 16 * lane);
-        r1 = ld16(j, (int64_t)b + 1024 + 16 * lane);
+        r0 = ld16o(j, n32, b + 16 * lane);
+        r1 = ld16o(j, n32, b + 1024 + 16 * lane);
     };
     auto refill_write = [&](int32_t b) {
         settle32(r0.x); settle32(r0.y); settle32(r0.z); settle32(r0.w);
@@ -704,8 +732,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             const int32_t gc = group_val(cand, gk);
             uint4 xa = make_uint4(0, 0, 0, 0), xb = xa;
             if (gk < K) {
-                xa = ld16(j, (int64_t)i + gk * S + 16 * gt);
-                if (gc >= 0) xb = ld16(j, (int64_t)gc + 16 * gt);
+                xa = ld16o(j, n32, i + gk * S + 16 * gt);
+                if (gc >= 0) xb = ld16o(j, n32, gc + 16 * gt);
             }
             const bool rf = (uint32_t)(i - wb) > 768u;          // the next batches' probes: window ahead
             if (rf) refill_issue(i);
@@ -797,7 +825,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             mc = gt16_decode(T16[mh], gt_code_of(F, mh), g);
             if (mc < 0 || pm_ - mc < 1 || pm_ - mc > 65535) mc = -1;
         }
-        const uint32_t vw = mc >= 0 ? ld_u32(j, mc) : 0u;
+        const uint32_t vw = mc >= 0 ? ld_u32o(j, n32, mc) : 0u;
         const int32_t inext = lane_val(pm_ + (int32_t)step, nb - 1);   // where a batch without a hit goes on
         const bool rf = (uint32_t)(i - wb) > 512u;              // the window for what follows either way
         if (rf) refill_issue(i);
