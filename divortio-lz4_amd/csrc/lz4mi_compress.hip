@@ -532,7 +532,7 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
 #define LZ4MI_DUPSLOT 1   // hit batches test for repeated hashes with an LDS slot before the DPP checks (A/B switch)
 #endif
 #ifndef LZ4MI_OFF32
-#define LZ4MI_OFF32 1   // batch encoder loads as 32-bit offsets from the block's base (A/B switch)
+#define LZ4MI_OFF32 0   // 1: batch encoder loads as 32-bit offsets from the block base (measured slower: 77.9 vs 74.9 ms)
 #endif
 // The batch encoder's loads (blocks < 2^31 bytes, lim = the block's length): 32-bit bounds
 // tests and a 32-bit unsigned offset from the block's (scalar) base, so the load takes the
