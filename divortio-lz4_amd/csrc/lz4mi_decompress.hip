@@ -609,6 +609,14 @@ struct WaveGen {
     }
 };
 
+// SeqInfo::rsrc (t_seq .w) of a sequence whose match source was mapped to finished output:
+// the source + kMemoBase when the whole match was mapped (remap_src follows it in one step for
+// later rows), + kSplitBase when only its part after a literal prefix was (0: not mapped).
+constexpr int32_t kMemoBase = 0x40000000, kSplitBase = 0x20000000;
+#ifndef LZ4MI_REMAP_MEMO
+#define LZ4MI_REMAP_MEMO 1   // 0: every hop through the sequences (A/B switch)
+#endif
+
 // A match source [rs, re) inside this table's output, mapped back through the
 // sequences that wrote it (out[y] = out[y - off] inside a match): 1 = it now
 // lies in output finished by earlier chunks, 2 = in sequence j's literal run
@@ -646,6 +654,16 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
             rs = ms;
         }
         if (re > ms + q.ml) return 0;
+#if LZ4MI_REMAP_MEMO
+        if (q.rsrc >= kMemoBase - 65536 && q.rsrc < kMemoBase + (1 << 27)) {
+            // sequence lo's match was itself mapped (by an earlier row) to finished output:
+            // follow that mapping in one step instead of hop by hop
+            const int32_t base = q.rsrc - kMemoBase - ms;
+            rs += base;
+            re += base;
+            continue;
+        }
+#endif
         rs -= q.off;
         re -= q.off;
     }
@@ -680,7 +698,7 @@ struct LaneMatchGen {
                 const int32_t ms = qi.out + qi.ll;
                 y = ms;
                 n = (ms + qi.ml > c.cap ? c.cap : ms + qi.ml) - ms;
-                src = (rbits >> bi) & 1u ? qi.rsrc : ms - qi.off;
+                src = (rbits >> bi) & 1u ? qi.rsrc - kMemoBase : ms - qi.off;
                 np = (n + 15) >> 4;
             }
         }
@@ -849,7 +867,7 @@ __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t 
                 const int32_t nl = i < 4 ? (int32_t)((nlit_pack >> (8 * i)) & 255u) : 0;   // split prefix
                 y = ms + nl;
                 n = (ms + q.ml > c.cap ? c.cap : ms + q.ml) - y;
-                src = (rbits >> i) & 1u ? q.rsrc : ms - q.off;
+                src = (rbits >> i) & 1u ? q.rsrc - (nl ? kSplitBase : kMemoBase) : ms - q.off;
             }
             const uint32_t np = rd ? (uint32_t)(n + 15) >> 4 : 0u;
             const uint32_t incl = wave_incl_scan(np, lane);
@@ -1565,7 +1583,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     if (r == 1 || r == 3) {
                         M.src = rs;
                         if (c.out_off + rs < 16) M.kind = R_BYTES;
-                        S.t_seq[k].w = (uint32_t)rs;
+                        S.t_seq[k].w = (uint32_t)(rs + (r == 3 ? kSplitBase : kMemoBase));
                         rbits |= 1u << i;
                     } else if (r == 2) {
                         ML = Run{M.y, M.n, li, 0, R_LDS};
