@@ -15,11 +15,16 @@ const reps = Number(process.argv[3] || 3);
 const depBytes = Math.min(input.length, Number(process.argv[4] || (16 << 20)));
 const BS = 4194304;
 const now = () => Number(process.hrtime.bigint()) / 1e9;
-const secs = (fn, n) => {
-    fn();                                 // warm-up
-    const t0 = now();
-    for (let r = 0; r < n; r++) fn();
-    return (now() - t0) / n;
+const secs = (fn, n) => {               // median of n timed calls after a warm-up call
+    fn();
+    const ts = [];
+    for (let r = 0; r < n; r++) {
+        const t0 = now();
+        fn();
+        ts.push(now() - t0);
+    }
+    ts.sort((a, b) => a - b);
+    return ts[(n - 1) >> 1];
 };
 const rate = (bytes, fn, n) => +(bytes / secs(fn, n) / 1e9).toFixed(3);
 const out = { bytes: input.length, routing: 'auto' };
@@ -51,8 +56,8 @@ for (const b of [1, 4, 16, 32, 64, 128]) {
     for (const side of ['gpu', 'host']) {
         LZ4.setRouting(side);
         let f = null;
-        cross.compress_ms[side].push(+(secs(() => { f = LZ4.compress(sub, null, BS, true, false); }, 2) * 1e3).toFixed(2));
-        cross.decompress_ms[side].push(+(secs(() => LZ4.decompress(f), 2) * 1e3).toFixed(2));
+        cross.compress_ms[side].push(+(secs(() => { f = LZ4.compress(sub, null, BS, true, false); }, 3) * 1e3).toFixed(2));
+        cross.decompress_ms[side].push(+(secs(() => LZ4.decompress(f), 3) * 1e3).toFixed(2));
     }
 }
 LZ4.setRouting('auto');
