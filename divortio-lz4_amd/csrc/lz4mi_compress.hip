@@ -358,11 +358,12 @@ __device__ void fast_literals(SH& F, FastOut& o, const CompJob& j, int lane, int
 
 
 
-// Sum over u < x of floor(u / 64): the miss-chain distance covered by the skip
-// steps (c + t) >> 6 is skip_sum(c + k) - skip_sum(c).
-__device__ __forceinline__ int64_t skip_sum(uint32_t x) {
-    const int64_t q = x >> 6, r = x & 63;
-    return 32 * q * (q - 1) + r * q;
+// The miss-chain distance covered by the skip steps (c + t) >> 6, t < k: the sum of floor(u / 64)
+// over u in [c, c + k), k < 64, in 32-bit arithmetic (floor(u / 64) is c >> 6, then at most once
+// more plus one).
+__device__ __forceinline__ int32_t skip_span(uint32_t c, uint32_t k) {
+    const uint32_t qa = c >> 6, b = c + k, e = (qa + 1) << 6;
+    return (int32_t)(k * qa + (b > e ? b - e : 0u));
 }
 
 // The general case of emit_seq (15+ literals or a match length field of 2+ extra bytes),
@@ -816,7 +817,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         // ================= miss batch: the next 64 probes of the miss chain, starting at i
         if (npend) emit_pending(load_lit());
         CPROF_COUNT(10, 1);
-        const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const int32_t pm_ = i + skip_span(c, (uint32_t)lane);
         const uint32_t step = (c + lane) >> 6;
         bool mact = pm_ < mflimit && (pm_ >> 15) == g;          // probes of the next epoch: the next batch
         const uint32_t mseq = seq_at(pm_, mact);
@@ -1090,7 +1091,7 @@ __device__ int64_t compress_block_chain2(const CompJob& j, ChainShared& F, int l
         }
         // ================= miss batch
         if (npend) emit_batch(load_lit());
-        const int32_t pm_ = i + (int32_t)(skip_sum(c + lane) - skip_sum(c));
+        const int32_t pm_ = i + skip_span(c, (uint32_t)lane);
         const uint32_t step = (c + lane) >> 6;
         bool mact = pm_ < mflimit;
         const uint32_t mseq = mact ? SrcR::u32(j, &r, pm_) : 0u;
