@@ -82,7 +82,7 @@ __device__ __forceinline__ int32_t group_val(int32_t v, int g) {
     }
     return r;
 #else
-    return __builtin_amdgcn_ds_bpermute(g << 2, v);   // (lane g's v: one LDS permute, no width masking)
+    return __shfl(v, g, kWave);
 #endif
 }
 
@@ -100,7 +100,7 @@ __device__ __forceinline__ uint32_t first_val(uint32_t v, uint64_t mm, int lane,
     }
     return r;
 #else
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((8 * (lane & 7) + ft) << 2, (int)v);
+    return __shfl(v, 8 * (lane & 7) + ft, kWave);
 #endif
 }
 
