@@ -169,3 +169,69 @@ def test_host_decoder_dependent_frames(manifest):
         assert pos == f["dec_len"] and "%08x" % lz4mi.xxh32(out[:pos]) == f["dec_xxh"], f
         done += 1
     assert done >= 4
+
+
+@pytest.mark.parametrize("gen", ["copy", "runs", "text", "tiles216", "random", "repetitive"])
+def test_host_decoder_matches_oracle_fuzz(gen):
+    """Differential check of the host decoder against the oracle's decoders (reference-exact and
+    spec) on seeded blocks, output offsets with bytes already in place (no stray writes), output
+    buffers shorter than the block (writes past the end vanish, or the reference's errors), and
+    byte-flipped inputs (statuses and every output byte, partial writes included)."""
+    rng = np.random.default_rng({"copy": 1, "runs": 2, "text": 3, "tiles216": 4, "random": 5, "repetitive": 6}[gen])
+    for seed in range(4):
+        n = int(rng.integers(1000, 120000))
+        src = O.generate(gen, 100 + seed, n)
+        comp = _host_block(src)
+        cases = [(comp, n, 0), (comp, n, int(rng.integers(1, 40))), (comp, max(1, n - int(rng.integers(1, 64))), 0)]
+        for _ in range(3):
+            bad = comp.copy()
+            for _ in range(int(rng.integers(1, 4))):
+                bad[int(rng.integers(0, bad.size))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+            cases.append((bad, n, int(rng.integers(0, 8))))
+        for blk, cap, off in cases:
+            for spec in (False, True):
+                base = rng.integers(0, 256, off + cap, dtype=np.uint8)
+                want_out = base.copy()
+                st, w, _ = O.decompress_block(blk, cap, out=want_out, out_off=off, js_compat=not spec)
+                got_out = base.copy()
+                try:
+                    got = lz4mi.host_decompress_raw(blk, 0, blk.size, got_out, off, spec=spec)
+                    got_st = 0
+                except lz4mi.Lz4miError as e:
+                    got, got_st = None, e.status
+                assert got_st == st, (gen, seed, spec, got_st, st)
+                if st == 0:
+                    assert got == w, (gen, seed, spec)
+                assert np.array_equal(got_out, want_out), (gen, seed, spec, off, cap)
+
+
+@pytest.mark.parametrize("gen", ["copy", "text", "tiles216", "random"])
+def test_host_encoder_matches_oracle_fuzz(gen):
+    """Differential check of the host encoder against the oracle's compressBlock restatement:
+    seeded sources, a start inside the source, a carried table, an output offset, outputs sized
+    to the bound and too small (the RangeError path and dropped stores): return value, every
+    output byte and the table after the call."""
+    rng = np.random.default_rng({"copy": 11, "text": 12, "tiles216": 13, "random": 14}[gen])
+    for seed in range(4):
+        n = int(rng.integers(2000, 150000))
+        src = O.generate(gen, 200 + seed, n)
+        start = int(rng.integers(0, 64))
+        length = n - start - int(rng.integers(0, 64))
+        table0 = np.zeros(16384, dtype=np.int32)
+        if seed & 1:   # a carried table: positions of an earlier call on the same source
+            O.compress_raw(src, np.zeros(O.compress_bound(start + 1) + 64, dtype=np.uint8), 0, max(start, 1), table0, 0)
+        for cap in (O.compress_bound(length) + 32, length // 3):
+            off = int(rng.integers(0, 16))
+            want_out = rng.integers(0, 256, cap, dtype=np.uint8)
+            got_out = want_out.copy()
+            want_t, got_t = table0.copy(), table0.copy()
+            want_st, want_n = O.compress_raw(src, want_out, start, length, want_t, off)   # -8: RangeError
+            try:
+                got_n, got_st = lz4mi.host_compress_raw(src, got_out, start, length, got_t, off), 0
+            except lz4mi.Lz4miError as e:
+                got_n, got_st = None, e.status
+            assert got_st == want_st, (gen, seed, cap, got_st, want_st)
+            if want_st == 0:
+                assert got_n == want_n, (gen, seed, cap)
+            assert np.array_equal(got_out, want_out), (gen, seed, cap)
+            assert np.array_equal(got_t, want_t), (gen, seed, cap)
