@@ -613,10 +613,6 @@ struct WaveGen {
 // the source + kMemoBase when the whole match was mapped (remap_src follows it in one step for
 // later rows), + kSplitBase when only its part after a literal prefix was (0: not mapped).
 constexpr int32_t kMemoBase = 0x40000000, kSplitBase = 0x20000000;
-#ifndef LZ4MI_REMAP_2PASS
-#define LZ4MI_REMAP_2PASS 1   // round 1's remap in two passes (short chains first) (A/B switch)
-#endif
-constexpr int kRemapPass1 = 2;   // hops of the first pass
 #ifndef LZ4MI_REMAP_MEMO
 #define LZ4MI_REMAP_MEMO 1   // 0: every hop through the sequences (A/B switch)
 #endif
@@ -630,12 +626,10 @@ constexpr int kRemapPass1 = 2;   // hops of the first pass
 // [rs, re) (finished output) — tiles216's usual reason for a later round (72 % of them).
 // S.nxt doubles as an output -> sequence map during round 1: entry b is the
 // sequence holding output O + (b << sh) (built by the kernel before round 1).
-// `hops` steps at most, then `exhausted` (4: resumable with the same rs/re/lds/nlit, `resume`).
 __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint32_t nseq, uint32_t sh, int32_t& rs,
-                                         int32_t& re, int32_t& lds, int32_t& nlit, bool split, int hops = 8,
-                                         bool resume = false, int exhausted = 0) {
-    if (!resume) nlit = 0;
-    for (int d = 0; d < hops; ++d) {
+                                         int32_t& re, int32_t& lds, int32_t& nlit, bool split) {
+    nlit = 0;
+    for (int d = 0; d < 8; ++d) {
         if (re <= (int32_t)c.O) return nlit ? 3 : 1;
         if (rs < (int32_t)c.O) return 0;
         uint32_t lo = S.nxt[(uint32_t)(rs - (int32_t)c.O) >> sh];   // last sequence starting at or before rs
@@ -673,7 +667,7 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
         rs -= q.off;
         re -= q.off;
     }
-    return exhausted;
+    return 0;
 }
 
 // Each lane copies its own non-periodic match runs from earlier output
@@ -1577,21 +1571,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     // the source is output of this table: map it back through the
                     // sequences that wrote it, else wait for a later round
                     int32_t rs = M.src, re = match_src_end(M), li = 0, nl = 0;
-                    int r = 0;
-                    if (M.kind == R_HIST && M.period == 0) {
-#if LZ4MI_REMAP_2PASS
-                        // two passes: the short chains first, their mappings recorded, then the
-                        // longer ones resumed, following those mappings in one step (the wave's
-                        // loop runs for its longest chain, so shortening the longest pays)
-                        r = remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4, kRemapPass1, false, 4);
-                        if (__ballot(r == 4)) {
-                            if (r == 1 || r == 3) S.t_seq[k].w = (uint32_t)(rs + (r == 3 ? kSplitBase : kMemoBase));
-                            if (r == 4) r = remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4, 8 - kRemapPass1, true);
-                        }
-#else
-                        r = remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4);
-#endif
-                    }
+                    const int r = (M.kind == R_HIST && M.period == 0)
+                                      ? remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4)
+                                      : 0;
                     if (r == 3) {   // literal prefix from the stage, the rest from finished output
                         ML = Run{M.y, nl, li, 0, R_LDS};
                         M.y += nl;
