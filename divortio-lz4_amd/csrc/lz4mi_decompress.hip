@@ -999,6 +999,19 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
     __syncthreads();
 }
 
+#ifndef LZ4MI_LIT_NT
+#define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
+#endif
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
+    const u32x4_nt t = __builtin_nontemporal_load((const u32x4_nt*)p);
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
+    const u32x4_nt t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, (u32x4_nt*)p);
+}
+
 // A long literal run (incompressible data: one run per block) copied global ->
 // global with 4 16-byte pieces per lane in flight (4 KiB per wave), enough to
 // keep HBM busy with one wave per block; the last piece overlaps its predecessor.
@@ -1008,6 +1021,18 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
     for (int32_t p0 = lane; p0 < np; p0 += kWave * 4) {
         const int32_t d0 = at(p0), d1 = at(p0 + kWave), d2 = at(p0 + 2 * kWave), d3 = at(p0 + 3 * kWave);
         uint4 v0, v1, v2, v3;
+#if LZ4MI_LIT_NT
+        // streamed once, never re-read soon: nontemporal, so they do not evict the history lines
+        // other blocks' matches read back from L2
+        v0 = ld16_nt(src + d0);
+        v1 = ld16_nt(src + d1);
+        v2 = ld16_nt(src + d2);
+        v3 = ld16_nt(src + d3);
+        st16_nt(dst + d0, v0);
+        st16_nt(dst + d1, v1);
+        st16_nt(dst + d2, v2);
+        st16_nt(dst + d3, v3);
+#else
         __builtin_memcpy(&v0, src + d0, 16);
         __builtin_memcpy(&v1, src + d1, 16);
         __builtin_memcpy(&v2, src + d2, 16);
@@ -1016,6 +1041,7 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
         out16(dst + d1, v1);
         out16(dst + d2, v2);
         out16(dst + d3, v3);
+#endif
     }
 }
 
