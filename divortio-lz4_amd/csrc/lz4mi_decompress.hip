@@ -46,6 +46,15 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
+#ifndef LZ4MI_STAGE_NT
+#define LZ4MI_STAGE_NT 0   // 1: the compressed stream staged with nontemporal loads (A/B switch)
+#endif
+#ifndef LZ4MI_PER_NT
+#define LZ4MI_PER_NT 0   // 1: long periodic runs stored nontemporally (A/B switch)
+#endif
+#ifndef LZ4MI_LIT_NT
+#define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
+#endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
@@ -73,6 +82,17 @@ namespace lz4mi {
 // policy: the written lines stay in L2 for the history reads that follow (nontemporal
 // stores, which skip L2, made tiles216 2x slower: 40.6 vs 20.5 ms).
 __device__ __forceinline__ void out16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+// 16 bytes read / written once (streamed: nontemporal, so they do not evict the history lines
+// the matches read back from L2)
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
+    const u32x4_nt t = __builtin_nontemporal_load((const u32x4_nt*)p);
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
+    const u32x4_nt t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, (u32x4_nt*)p);
+}
 
 #if LZ4MI_PROFILE
 __device__ unsigned long long g_prof[24];
@@ -184,7 +204,13 @@ __device__ __forceinline__ uint4 stage16(const uint32_t* stage, int32_t idx) {
 // 16 compressed bytes at block-relative r0 (zero past the block end).
 __device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + 16 <= c.in_len) __builtin_memcpy(&v, c.blk + r0, 16);
+    if (r0 + 16 <= c.in_len) {
+#if LZ4MI_STAGE_NT
+        v = ld16_nt(c.blk + r0);
+#else
+        __builtin_memcpy(&v, c.blk + r0, 16);
+#endif
+    }
     else if (r0 < c.in_len) v = load16_tail(c.blk, r0, c.in_len);
     return v;
 }
@@ -977,7 +1003,13 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
             const bool last = d0 > dl;
             const int32_t d = last ? dl : d0;
             const int32_t ph = (last ? d % per : r) - s0;
-            if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, ph));
+            if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) {
+#if LZ4MI_PER_NT
+                st16_nt(c.dst + R.y + d, stage16(B.w, ph));
+#else
+                out16(c.dst + R.y + d, stage16(B.w, ph));
+#endif
+            }
             r += step;
             if (r >= per) r -= per;
         }
@@ -999,18 +1031,6 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
     __syncthreads();
 }
 
-#ifndef LZ4MI_LIT_NT
-#define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
-#endif
-typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4), aligned(1)));
-__device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
-    const u32x4_nt t = __builtin_nontemporal_load((const u32x4_nt*)p);
-    return make_uint4(t.x, t.y, t.z, t.w);
-}
-__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
-    const u32x4_nt t = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(t, (u32x4_nt*)p);
-}
 
 // A long literal run (incompressible data: one run per block) copied global ->
 // global with 4 16-byte pieces per lane in flight (4 KiB per wave), enough to
