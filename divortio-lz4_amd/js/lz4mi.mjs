@@ -850,10 +850,9 @@ export class LZ4Decoder {
     _decodeIndependent(blocks) {
         const nb = blocks.length, cap = this.blockMax || BLOCK_MAX_SIZES[7];
         if (hostRoute(nb, HOST_MAX_BLOCKS_DECOMPRESS)) {
-            return blocks.map((b) => {
-                const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
-                return ws.slice(0, native.decompressBlockHost(b.data, 0, b.data.length, ws, 0, null, decodeFlags));
-            });
+            const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);   // the reference's 4 MiB workspace, reused
+            return blocks.map((b) => ws.slice(0, native.decompressBlockHost(b.data, 0, b.data.length, ws, 0, null,
+                decodeFlags)));
         }
         let total = 0;
         for (const b of blocks) total += b.data.length;
