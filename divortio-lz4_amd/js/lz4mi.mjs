@@ -486,8 +486,8 @@ function batchDirect(data, blocks, result, dict, bmax) {
         if (status[b] === native.ERR_CROSS_BLOCK) {
             // reads bytes of an earlier block (dependent frame, or the F1 rewrite
             // at a block start): every earlier block is final now, decode it alone
-            try {
-                outLen[b] = native.decompressBlock(data, inOff[b], inLen[b], result, outOff[b], dict, decodeFlags);
+            try {   // (one block: the host decoder unless routing 'gpu')
+                outLen[b] = decompressRaw(data, inOff[b], inLen[b], result, outOff[b], dict);
             } catch (e) {
                 return false;
             }
@@ -875,7 +875,7 @@ export class LZ4Decoder {
                 // a back-reference (or the F1 rewrite) before the block's start: decode it alone,
                 // into a fresh workspace, which also raises the reference's error if it has one
                 const ws = new Uint8Array(BLOCK_MAX_SIZES[7]);
-                const w = native.decompressBlock(blocks[k].data, 0, blocks[k].data.length, ws, 0, null, decodeFlags);
+                const w = decompressRaw(blocks[k].data, 0, blocks[k].data.length, ws, 0, null);
                 res.push(ws.slice(0, w));
             } else {
                 res.push(out.slice(outOff[k], outOff[k] + outLen[k]));
