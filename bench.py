@@ -351,7 +351,7 @@ def napi_e2e(batch, nblocks=128):
     path = os.path.join(tempfile.gettempdir(), f"lz4mi_napi_{os.getpid()}.bin")
     try:
         batch.raw[:nblocks * BLOCK].cpu().numpy().tofile(path)
-        r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "tools", "napi_e2e.mjs"), path, "3"],
+        r = subprocess.run(["node", "--no-warnings", "--expose-gc", os.path.join(ROOT, "tools", "napi_e2e.mjs"), path, "3"],
                            capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             return {"error": r.stderr[-500:]}

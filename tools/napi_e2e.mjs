@@ -15,7 +15,9 @@ const reps = Number(process.argv[3] || 3);
 const depBytes = Math.min(input.length, Number(process.argv[4] || (16 << 20)));
 const BS = 4194304;
 const now = () => Number(process.hrtime.bigint()) / 1e9;
+const gc = globalThis.gc || (() => {});   // (node --expose-gc: large results of earlier calls collected first)
 const secs = (fn, n) => {               // median of n timed calls after a warm-up call
+    gc();
     fn();
     const ts = [];
     for (let r = 0; r < n; r++) {

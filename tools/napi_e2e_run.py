@@ -13,7 +13,7 @@ import oracle as O  # noqa: E402  (generator only: the input bytes)
 path = "/tmp/lz4mi_e2e_%d.bin" % os.getpid()
 np.concatenate([O.generate("tiles216", 1 + i, 4 << 20) for i in range(128)]).tofile(path)
 try:
-    r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "tools", "napi_e2e.mjs"), path, "3"],
+    r = subprocess.run(["node", "--no-warnings", "--expose-gc", os.path.join(ROOT, "tools", "napi_e2e.mjs"), path, "3"],
                        capture_output=True, text=True, timeout=280)
     print(r.stdout.strip()[-3000:])
     print(r.stderr[-800:], file=sys.stderr)
