@@ -285,8 +285,9 @@ static napi_value compress_chain_impl(napi_env env, napi_callback_info info, int
         napi_throw_type_error(env, NULL, "lz4mi: hashTable must be an Int32Array(16384)");
         return NULL;
     }
-    if (start < 0 || len < 0 || bs <= 0 || bs > LZ4MI_MAX_BLOCK || !in_bounds((uint64_t)start, (uint64_t)len, src.length))
-        return throw_status(env, LZ4MI_ERR_ARG);
+    if (start < 0 || len < 0 || bs <= 0 || bs > LZ4MI_MAX_BLOCK || start + len > INT32_MAX ||
+        !in_bounds((uint64_t)start, (uint64_t)len, src.length))
+        return throw_status(env, LZ4MI_ERR_ARG);   /* (positions are int32 in the reference's table) */
     const uint32_t n = (uint32_t)((len + bs - 1) / bs);
     if (!u32_array(env, &clen, n, 0, "compLen")) return NULL;
     uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
