@@ -605,7 +605,8 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     auto load_lit = [&]() -> uint32_t {
         uint32_t litv = 0;
         const int32_t lit0 = lane_val(pd_p, 0) - anchor;
-        const bool ld = lit0 > 0 && lit0 < 15 && lane >= 1 && lane <= lit0;
+        if (lit0 <= 0 || lit0 >= 15) return 0u;                // (uniform: most batches have no literals)
+        const bool ld = lane >= 1 && lane <= lit0;
         const int32_t ow = anchor - wb;
         if (ow >= 0 && ow + lit0 + 4 <= kWinBytes) {          // from the window
             const int32_t q = ow + lane - 1;
