@@ -207,7 +207,7 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
     decoder = F.DeviceDecoder(stream_obj)
     # warm-up: the same frame without checksums (allocations, scratch growth, first launches)
     w = F.compress_frame_sharded(raw, BLOCK, content_checksum=False, add_content_size=True, codec=codec)
-    w = F.decompress_frame_sharded(w, verify_checksum=False, decoder=decoder, device=dev, gather=True)
+    w = F.decompress_frame_sharded(w, verify_checksum=False, decoder=decoder, device=dev, gather=True, zero_copy=True)
     del w
     torch.cuda.synchronize()
     if dist is not None:
@@ -222,14 +222,14 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
         dist.barrier()
     ts = {}     # sharded result (gather=False): each rank keeps its decoded run
     t0 = time.perf_counter()
-    part = F.decompress_frame_sharded(frame, verify_checksum=True, decoder=decoder, timings=ts, device=dev, gather=False)
+    part = F.decompress_frame_sharded(frame, verify_checksum=True, decoder=decoder, timings=ts, device=dev, gather=False, zero_copy=True)
     d_sharded = time.perf_counter() - t0
     del part
     if dist is not None:
         dist.barrier()
     td = {}
     t0 = time.perf_counter()
-    out = F.decompress_frame_sharded(frame, verify_checksum=True, decoder=decoder, timings=td, device=dev, gather=True)
+    out = F.decompress_frame_sharded(frame, verify_checksum=True, decoder=decoder, timings=td, device=dev, gather=True, zero_copy=True)
     d_total = time.perf_counter() - t0
     total_raw = world * n * BLOCK
     ok = torch.tensor([1], dtype=torch.int32, device=dev)

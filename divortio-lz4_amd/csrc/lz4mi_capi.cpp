@@ -213,6 +213,7 @@ const char* lz4mi_status_message(int32_t s) {
         case LZ4MI_ERR_HIP: return "lz4mi: HIP runtime error";
         case LZ4MI_ERR_ARG: return "lz4mi: invalid argument";
         case LZ4MI_ERR_NO_DEVICE: return "lz4mi: no gfx950 (MI355X) device available";
+        case LZ4MI_ERR_DEVICE_BOUND: return "lz4mi: library already bound to another device (one device per process)";
         default: return "lz4mi: unknown status";
     }
 }
@@ -254,7 +255,7 @@ static int32_t init_locked(int32_t device) {
     if (g_ctx.device == device) return LZ4MI_OK;
     // the context is bound to one device for the life of the process: another thread may
     // hold a StreamCtx* (and its lock) of this device, so nothing of it is ever released
-    if (g_ctx.device >= 0) return LZ4MI_ERR_ARG;
+    if (g_ctx.device >= 0) return LZ4MI_ERR_DEVICE_BOUND;
     LZ4MI_TRY(hipSetDevice(device));
     LZ4MI_TRY(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     g_ctx.device = device;
@@ -467,7 +468,8 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
 int64_t lz4mi_compress_block_table(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
                                    int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off, uint32_t flags,
                                    void* stream) {
-    if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table || out_off < 0)
+    if (src_start < 0 || src_len < 0 || (uint64_t)src_start + (uint64_t)src_len > src_total || !table || out_off < 0 ||
+        (uint64_t)src_start + (uint64_t)src_len > INT32_MAX)   // int32 positions (table values position + 1)
         return LZ4MI_ERR_ARG;
     if (flags & LZ4MI_DEVICE_PTRS) return LZ4MI_ERR_ARG;   // host-only entry point (see header)
     {
@@ -721,6 +723,18 @@ int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off,
     if (!(flags & LZ4MI_DEVICE_PTRS) || !frame || !info || (cap_blocks && (!pay_off || !size_word)))
         return LZ4MI_ERR_ARG;
     LZ4MI_TRY(lz4mi_launch_frame_index(frame, len, cap_blocks, pay_off, size_word, info, pick_stream(stream)));
+    return LZ4MI_OK;
+}
+
+int32_t lz4mi_copy_stored_blocks(const uint8_t* frame, uint64_t len, const uint64_t* in_off, const uint32_t* n,
+                                 const uint64_t* out_off, uint8_t* out, uint64_t out_cap, uint32_t nblocks,
+                                 uint32_t flags, void* stream) {
+    DeviceGuard dg;
+    if (dg.status()) return dg.status();
+    if (!(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
+    if (nblocks == 0) return LZ4MI_OK;
+    if (!frame || !in_off || !n || !out_off || !out) return LZ4MI_ERR_ARG;
+    LZ4MI_TRY(lz4mi_launch_frame_stored(frame, len, in_off, n, out_off, out, out_cap, nblocks, pick_stream(stream)));
     return LZ4MI_OK;
 }
 

@@ -46,30 +46,26 @@
 
 #ifndef LZ4MI_PERIODIC_LDS
 #define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
-#ifndef LZ4MI_STAGE_NT
-#define LZ4MI_STAGE_NT 0   // 1: the compressed stream staged with nontemporal loads (A/B switch)
-#endif
-#ifndef LZ4MI_PER_NT
-#define LZ4MI_PER_NT 0   // 1: long periodic runs stored nontemporally (A/B switch)
 #endif
 #ifndef LZ4MI_LIT_NT
 #define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
 #endif
+#ifndef LZ4MI_LL_DEPTH
+#define LZ4MI_LL_DEPTH 4   // long literal runs: 16-byte pieces per lane in flight per step (A/B switch)
+#endif
+#ifndef LZ4MI_LL_SLEEP
+#define LZ4MI_LL_SLEEP 0   // long literal runs: s_sleep argument after every step (pacing A/B switch)
+#endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
-#endif
 #endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
 #endif
 
-#ifndef LZ4MI_PIECES
-#define LZ4MI_PIECES 1   // ready matches copied piece-parallel (piece_pipe); 0: one lane per match (A/B switch)
-#endif
-
-#ifndef LZ4MI_DEFER
-#define LZ4MI_DEFER 0    // round 1's last piece batch stored during the next chunk's parse (A/B switch)
+#ifndef LZ4MI_TIMELINE
+#define LZ4MI_TIMELINE 0   // diagnostic build (tools/timeline.py): every block's start / end time, CU, XCD
 #endif
 
 #ifndef LZ4MI_PROFILE
@@ -94,6 +90,12 @@ __device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
     __builtin_nontemporal_store(t, (u32x4_nt*)p);
 }
 
+#if LZ4MI_TIMELINE
+constexpr uint32_t kTlMax = 16384;
+__device__ unsigned long long g_tl[2 * kTlMax];   // per block: start, end (s_memrealtime, 100 MHz)
+__device__ unsigned int g_tl_id[2 * kTlMax];      // per block: HW_ID (wave, SIMD, CU, SH, SE), XCC_ID
+#endif
+
 #if LZ4MI_PROFILE
 __device__ unsigned long long g_prof[24];
 #define PROF(i)                              \
@@ -117,7 +119,6 @@ constexpr uint32_t kWarm = 512;               // speculative walks start this fa
 constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
-constexpr int kB = 4;                         // pieces per lane per pipeline stage (lane-parallel runs)
 constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 256;               // longer runs are written by the whole wave (128: tiles216 +1.8 %)
@@ -204,13 +205,7 @@ __device__ __forceinline__ uint4 stage16(const uint32_t* stage, int32_t idx) {
 // 16 compressed bytes at block-relative r0 (zero past the block end).
 __device__ __forceinline__ uint4 stage_piece(const Ctx& c, int64_t r0) {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + 16 <= c.in_len) {
-#if LZ4MI_STAGE_NT
-        v = ld16_nt(c.blk + r0);
-#else
-        __builtin_memcpy(&v, c.blk + r0, 16);
-#endif
-    }
+    if (r0 + 16 <= c.in_len) __builtin_memcpy(&v, c.blk + r0, 16);
     else if (r0 < c.in_len) v = load16_tail(c.blk, r0, c.in_len);
     return v;
 }
@@ -590,7 +585,7 @@ __device__ __forceinline__ bool any_slot(const Slot (&s)[NB]) {
 
 // Software-pipelined copy: the loads of stage n+1 are issued before the stores
 // of stage n, so no load waits behind a store it does not depend on (gfx9
-// counts loads and stores in one in-order vmcnt). Gen::fill(Slot (&)[kB])
+// counts loads and stores in one in-order vmcnt). Gen::fill(Slot (&)[NB])
 // hands out this lane's next pieces (sources already complete).
 template <uint32_t KIND, bool TWO, int NB, class Gen>
 __device__ __forceinline__ void pipe(const Ctx& c, DecShared& S, Gen& g) {
@@ -696,57 +691,11 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
     return 0;
 }
 
-// Each lane copies its own non-periodic match runs from earlier output
-// (sequences 64 i + lane for every bit i of `bits`), software-pipelined like
-// pipe() with a lean slot (every piece is one 16-byte window): y, source, width.
+// One 16-byte piece of a match copy: y, source, width.
 struct LSlot {
     int32_t y, a;
     uint32_t w;   // 0 = none
 };
-
-struct LaneMatchGen {
-    const Ctx& c;
-    const DecShared& S;
-    uint32_t bits, rbits;   // rbits: the source was remapped (SeqInfo::rsrc)
-    int lane, q, np;
-    int32_t y, n, src;
-    // One batch = up to NB pieces of ONE run (runs are >= 16 bytes here, so
-    // every piece is a full 16-byte window; the last one overlaps its predecessor).
-    template <int NB>
-    __device__ __forceinline__ void fill(LSlot (&s)[NB]) {
-        if (q >= np) {
-            np = 0;
-            q = 0;
-            if (bits) {
-                const uint32_t bi = __builtin_ctz(bits), k = 64u * bi + lane;
-                bits &= bits - 1;
-                const SeqInfo qi = seq_info(S, k);
-                const int32_t ms = qi.out + qi.ll;
-                y = ms;
-                n = (ms + qi.ml > c.cap ? c.cap : ms + qi.ml) - ms;
-                src = (rbits >> bi) & 1u ? qi.rsrc - kMemoBase : ms - qi.off;
-                np = (n + 15) >> 4;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int32_t d = 16 * (q + j) < n - 16 ? 16 * (q + j) : n - 16;
-            s[j] = LSlot{y + d, src + d, q + j < np ? 16u : 0u};
-        }
-        q += NB;
-    }
-};
-
-template <int NB>
-__device__ __forceinline__ void lane_load(const Ctx& c, const LSlot (&s)[NB], uint4 (&A)[NB]) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        if (s[j].w) {
-            const u32x4_t t = *(const u32x4_t*)(c.dst + s[j].a);
-            A[j] = make_uint4(t.x, t.y, t.z, t.w);
-        }
-    }
-}
 
 template <int NB>
 __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSlot (&s)[NB], const uint4 (&A0)[NB]) {
@@ -764,40 +713,6 @@ __device__ __forceinline__ void lane_store(const Ctx& c, DecShared& S, const LSl
             continue;
         }
         out16(c.dst + s[j].y, A[j]);
-    }
-}
-
-template <int NB>
-__device__ __forceinline__ bool any_lslot(const LSlot (&s)[NB]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) m |= s[j].w;
-    return m != 0;
-}
-
-template <int NB, class Gen>
-__device__ __forceinline__ void lane_pipe(const Ctx& c, DecShared& S, Gen& g) {
-    // (as pipe(): no load left in flight at the exit)
-    LSlot s0[NB], s1[NB];
-    uint4 a0[NB], a1[NB];
-    g.template fill<NB>(s0);
-    if (!__ballot(any_lslot<NB>(s0))) return;
-    lane_load<NB>(c, s0, a0);
-    for (;;) {
-        g.template fill<NB>(s1);
-        if (!__ballot(any_lslot<NB>(s1))) {
-            lane_store<NB>(c, S, s0, a0);
-            return;
-        }
-        lane_load<NB>(c, s1, a1);
-        lane_store<NB>(c, S, s0, a0);
-        g.template fill<NB>(s0);
-        if (!__ballot(any_lslot<NB>(s0))) {
-            lane_store<NB>(c, S, s1, a1);
-            return;
-        }
-        lane_load<NB>(c, s0, a0);
-        lane_store<NB>(c, S, s1, a1);
     }
 }
 
@@ -851,29 +766,10 @@ struct PieceGen {
     }
 };
 
-// Round 1's last piece batch with its loads in flight and its stores not yet issued:
-// they go out during the next chunk's parse (after its walks), so the batch's load round
-// trip overlaps the parse instead of ending the chunk. Only for a chunk that needs nothing
-// after round 1 (no later rounds, no cut sequence, no F1 check: nothing reads its output
-// before the next chunk's output phase, whose opening wait covers these stores).
-struct Deferred {
-    uint4 v[kPieceBatch];
-    int32_t y[kPieceBatch];   // -1: empty slot
-    bool any;
-};
-
-__device__ __forceinline__ void flush_deferred(const Ctx& c, Deferred& d) {
-#pragma unroll
-    for (int j = 0; j < kPieceBatch; ++j)
-        if (d.y[j] >= 0) out16(c.dst + d.y[j], d.v[j]);
-    d.any = false;
-}
-
 // The matches of sequences 64 i + lane for every bit i of `ready` (sources: SeqInfo::rsrc
-// where `rbits` says so), two sequence rows per batch. With `dfr` the last batch's stores
-// are deferred (Deferred above).
+// where `rbits` says so), two sequence rows per batch.
 __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t ready, uint32_t rbits, int lane,
-                                           uint32_t nseq, Deferred& dfr, bool defer, uint32_t nlit_pack) {
+                                           uint32_t nseq, uint32_t nlit_pack) {
     PEnt* L = reinterpret_cast<PEnt*>(S.pme);
     uint64_t* bm = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(S.pme) + 2 * kWave * sizeof(PEnt));
     for (uint32_t i0 = 0; 64u * i0 < nseq; i0 += 2) {
@@ -920,15 +816,6 @@ __device__ __forceinline__ void piece_pipe(const Ctx& c, DecShared& S, uint32_t 
             for (int j = 0; j < kPieceBatch; ++j) {
                 const u32x4_t t = *(const u32x4_t*)(c.dst + (sl[j].w ? sl[j].a : 0));
                 v[j] = make_uint4(t.x, t.y, t.z, t.w);
-            }
-            if (defer && 64u * g.t >= P && 64u * (i0 + 2) >= nseq) {   // the chunk's last batch
-#pragma unroll
-                for (int j = 0; j < kPieceBatch; ++j) {
-                    dfr.v[j] = v[j];
-                    dfr.y[j] = sl[j].w ? sl[j].y : -1;
-                }
-                dfr.any = true;
-                break;
             }
             lane_store<kPieceBatch>(c, S, sl, v);
         }
@@ -1004,11 +891,7 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
             const int32_t d = last ? dl : d0;
             const int32_t ph = (last ? d % per : r) - s0;
             if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) {
-#if LZ4MI_PER_NT
-                st16_nt(c.dst + R.y + d, stage16(B.w, ph));
-#else
                 out16(c.dst + R.y + d, stage16(B.w, ph));
-#endif
             }
             r += step;
             if (r >= per) r -= per;
@@ -1033,35 +916,31 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
 
 
 // A long literal run (incompressible data: one run per block) copied global ->
-// global with 4 16-byte pieces per lane in flight (4 KiB per wave), enough to
-// keep HBM busy with one wave per block; the last piece overlaps its predecessor.
+// global with LZ4MI_LL_DEPTH 16-byte pieces per lane in flight (4 KiB per wave at 4),
+// enough to keep HBM busy with one wave per block; the last piece overlaps its predecessor.
 __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, int32_t n, int lane) {
+    constexpr int D = LZ4MI_LL_DEPTH;
     const int32_t np = (n + 15) >> 4;
     auto at = [&](int32_t p) { return 16 * p < n - 16 ? 16 * p : n - 16; };   // past the end: the last piece again
-    for (int32_t p0 = lane; p0 < np; p0 += kWave * 4) {
-        const int32_t d0 = at(p0), d1 = at(p0 + kWave), d2 = at(p0 + 2 * kWave), d3 = at(p0 + 3 * kWave);
-        uint4 v0, v1, v2, v3;
+    for (int32_t p0 = lane; p0 < np; p0 += kWave * D) {
+        int32_t d[D];
+        uint4 v[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) d[j] = at(p0 + j * kWave);
 #if LZ4MI_LIT_NT
         // streamed once, never re-read soon: nontemporal, so they do not evict the history lines
         // other blocks' matches read back from L2
-        v0 = ld16_nt(src + d0);
-        v1 = ld16_nt(src + d1);
-        v2 = ld16_nt(src + d2);
-        v3 = ld16_nt(src + d3);
-        st16_nt(dst + d0, v0);
-        st16_nt(dst + d1, v1);
-        st16_nt(dst + d2, v2);
-        st16_nt(dst + d3, v3);
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[j] = ld16_nt(src + d[j]);
+#pragma unroll
+        for (int j = 0; j < D; ++j) st16_nt(dst + d[j], v[j]);
 #else
-        __builtin_memcpy(&v0, src + d0, 16);
-        __builtin_memcpy(&v1, src + d1, 16);
-        __builtin_memcpy(&v2, src + d2, 16);
-        __builtin_memcpy(&v3, src + d3, 16);
-        out16(dst + d0, v0);
-        out16(dst + d1, v1);
-        out16(dst + d2, v2);
-        out16(dst + d3, v3);
+#pragma unroll
+        for (int j = 0; j < D; ++j) __builtin_memcpy(&v[j], src + d[j], 16);
+#pragma unroll
+        for (int j = 0; j < D; ++j) out16(dst + d[j], v[j]);
 #endif
+        if (LZ4MI_LL_SLEEP) __builtin_amdgcn_s_sleep(LZ4MI_LL_SLEEP);
     }
 }
 
@@ -1248,6 +1127,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const int lane = threadIdx.x;
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
+#if LZ4MI_TIMELINE
+    const uint64_t tl_t0 = wall_clock64();
+#endif
 
     // the block's scalars in SGPRs (readfirstlane): as VGPRs the compiler would keep
     // per-lane copies of values derived from them and spill those to scratch
@@ -1267,8 +1149,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     int32_t status = 0;
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
     bool have_pf = false;
-    Deferred dfr;                          // round 1's last piece batch, stored during the next parse
-    dfr.any = false;
     int64_t pf_at = -1;                    // compressed position pf0/pf1 were loaded from
 #if LZ4MI_PROFILE
     uint64_t prof[24] = {0};
@@ -1386,12 +1266,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         if (nE >= seg1) vis = 0;
         else vis &= ~((1u << (nE - seg0)) - 1u);
         tail = lane_of(x, kWave - 1);   // where the chain leaves the chunk
-        if (dfr.any) flush_deferred(c, dfr);   // the previous chunk's last pieces (their loads are back by now)
-#pragma unroll
-        for (int j = 0; j < kPieceBatch; ++j) {   // (the old values end here: not live through this chunk)
-            dfr.v[j] = make_uint4(0, 0, 0, 0);
-            dfr.y[j] = -1;
-        }
         if (tail > (uint32_t)kLim && tail < kEnd) tail = kStop;   // (fast table: raw positions past the window)
         }
         (void)seg1;
@@ -1618,7 +1492,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     // sequences that wrote it, else wait for a later round
                     int32_t rs = M.src, re = match_src_end(M), li = 0, nl = 0;
                     const int r = (M.kind == R_HIST && M.period == 0)
-                                      ? remap_src(c, S, nseq, msh, rs, re, li, nl, LZ4MI_PIECES && i < 4)
+                                      ? remap_src(c, S, nseq, msh, rs, re, li, nl, i < 4)
                                       : 0;
                     if (r == 3) {   // literal prefix from the stage, the rest from finished output
                         ML = Run{M.y, nl, li, 0, R_LDS};
@@ -1652,17 +1526,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_round1(S));
             PROF(18);
         }
-#if LZ4MI_PIECES
-        piece_pipe(c, S, ready, rbits, lane, nseq, dfr, LZ4MI_DEFER && !cut && !a.f1check && __ballot(pend != 0) == 0,
-                   nlit_pack);
-        if (dfr.any) goto chunk_done;   // nothing else to write (and the deferred batch stays out of
-                                        // the rounds' registers)
-#else
-        {
-            LaneMatchGen g{c, S, ready, rbits, lane, 0, 0, 0, 0, 0};
-            lane_pipe<kB>(c, S, g);
-        }
-#endif
+        piece_pipe(c, S, ready, rbits, lane, nseq, nlit_pack);
         PROF(19);
         for (; LZ4MI_ABLATE != 6;) {                           // rounds 2, 3, ...
             uint32_t np = 0;
@@ -1710,14 +1574,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 if (M.kind != R_NONE && !longM && !fastM) lane_slow_run(c, S, M);
                 for (uint64_t mm = __ballot(longM); mm; mm &= mm - 1) wave_run(c, S, lane, shfl_run(M, __builtin_ctzll(mm)), pat_rounds(S));
             }
-#if LZ4MI_PIECES
-            piece_pipe(c, S, ready, 0u, lane, nseq, dfr, false, 0u);
-#else
-            {
-                LaneMatchGen g{c, S, ready, 0u, lane, 0, 0, 0, 0, 0};
-                lane_pipe<kB>(c, S, g);
-            }
-#endif
+            piece_pipe(c, S, ready, 0u, lane, nseq, 0u);
             __syncthreads();
         }
         PROF(6);
@@ -1762,7 +1619,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             }
         }
 #endif
-    chunk_done:
         c.O = tab_hi;
         if (cut) {
             c.O += cll + cml;
@@ -1775,7 +1631,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         __syncthreads();
         PROF(8);
     }
-    if (dfr.any) flush_deferred(c, dfr);   // the last chunk's deferred pieces
 #if LZ4MI_PROFILE
     if (lane == 0)
         for (int i = 0; i < 24; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
@@ -1784,6 +1639,19 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         a.status[b] = status;
         a.out_len[b] = status ? 0u : (uint32_t)c.O;
     }
+#if LZ4MI_TIMELINE
+    wait_vmem();
+    const uint64_t tl_t1 = wall_clock64();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && b < kTlMax) {
+        g_tl[2 * b] = tl_t0;
+        g_tl[2 * b + 1] = tl_t1;
+        g_tl_id[2 * b] = hw;
+        g_tl_id[2 * b + 1] = xcc;
+    }
+#endif
 }
 
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block(a); }
@@ -1796,6 +1664,15 @@ extern "C" int lz4mi_debug_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4mi::g_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
     unsigned long long z[24] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(lz4mi::g_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#if LZ4MI_TIMELINE
+// The last launch's per-block timeline (n <= kTlMax blocks): t[2b] start, t[2b+1] end, id[2b] HW_ID, id[2b+1] XCC_ID.
+extern "C" int lz4mi_debug_timeline(unsigned long long* t, unsigned int* id, unsigned int n) {
+    if (n > lz4mi::kTlMax) n = lz4mi::kTlMax;
+    if (hipMemcpyFromSymbol(t, HIP_SYMBOL(lz4mi::g_tl), sizeof(unsigned long long) * 2 * n) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(id, HIP_SYMBOL(lz4mi::g_tl_id), sizeof(unsigned int) * 2 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 

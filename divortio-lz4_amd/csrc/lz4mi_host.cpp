@@ -12,6 +12,7 @@
 // (c++ >> 6), no inserts inside matches, output writes past the buffer dropped as a
 // typed array drops them, and the RangeError output.set() throws for a literal run of
 // more than 64 bytes that does not fit (blockCompress.js:100, :198).
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -75,8 +76,8 @@ inline int64_t common(const uint8_t* a, const uint8_t* b, int64_t lim) {
 // One compressBlock call. Returns bytes written (dIndex - outputOffset) or LZ4MI_ERR_RANGE.
 int64_t compress_block(const uint8_t* src, int32_t start, int32_t len, int32_t* T, Out& o) {
     const int64_t out0 = o.d;
-    const int32_t end = start + len;
-    const int32_t mflimit = end - 12, matchlimit = end - 5;
+    const int64_t end = (int64_t)start + len;   // callers keep start + len <= INT32_MAX
+    const int64_t mflimit = end - 12, matchlimit = end - 5;
     int32_t i = start, anchor = start;
     uint32_t c = 67;
     while (i < mflimit) {
@@ -105,7 +106,7 @@ int64_t compress_block(const uint8_t* src, int32_t start, int32_t len, int32_t* 
         i = (int32_t)e;
         anchor = (int32_t)e;
     }
-    const int64_t lit = end - anchor;
+    const int64_t lit = end - anchor;   // >= 0: anchor <= end
     o.put(lit >= 15 ? 0xF0u : (uint32_t)lit << 4);
     if (lit >= 15) o.len_ext(lit - 15);
     if (!o.lits(src + anchor, lit)) return LZ4MI_ERR_RANGE;
@@ -118,8 +119,10 @@ extern "C" {
 
 int64_t lz4mi_host_compress_block(const uint8_t* src, uint64_t src_total, int32_t src_start, int32_t src_len,
                                   int32_t* table, uint8_t* out, uint64_t out_total, int32_t out_off) {
+    // positions are int32 (the table holds position + 1): start + len must stay below 2^31
     if ((!src && src_total) || !table || src_start < 0 || src_len < 0 ||
-        (uint64_t)src_start + (uint64_t)src_len > src_total || out_off < 0 || (!out && out_total))
+        (uint64_t)src_start + (uint64_t)src_len > src_total || (uint64_t)src_start + (uint64_t)src_len > INT32_MAX ||
+        out_off < 0 || (!out && out_total))
         return LZ4MI_ERR_ARG;
     Out o{out, (int64_t)out_total, out_off};
     return compress_block(src, src_start, src_len, table, o);
@@ -129,7 +132,7 @@ int32_t lz4mi_host_compress_chain(const uint8_t* src, uint64_t src_total, int32_
                                   int32_t block_size, int32_t* table, uint8_t* out, const uint64_t* out_off,
                                   uint32_t* comp_len) {
     if ((!src && src_total) || !table || !out || !out_off || !comp_len || start < 0 || len < 0 || block_size <= 0 ||
-        (uint64_t)start + (uint64_t)len > src_total)
+        (uint64_t)start + (uint64_t)len > src_total || (uint64_t)start + (uint64_t)len > INT32_MAX)
         return LZ4MI_ERR_ARG;
     const int64_t nb = ((int64_t)len + block_size - 1) / block_size;
     for (int64_t b = 0; b < nb; ++b) {

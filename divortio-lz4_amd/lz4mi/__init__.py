@@ -21,7 +21,7 @@ OK = 0
 ERR_OUTPUT_TOO_SMALL, ERR_MALFORMED, ERR_OFFSET0, ERR_DICT_OOB = -1, -2, -3, -4
 ERR_MAGIC, ERR_VERSION, ERR_CHECKSUM, ERR_RANGE, ERR_CROSS_BLOCK = -5, -6, -7, -8, -9
 ERR_BLOCK_CHECKSUM = -10
-ERR_HIP, ERR_ARG, ERR_NO_DEVICE = -100, -101, -102
+ERR_HIP, ERR_ARG, ERR_NO_DEVICE, ERR_DEVICE_BOUND = -100, -101, -102, -103
 
 DEVICE_PTRS = 0x1
 JS_COMPAT = 0x2
@@ -39,7 +39,8 @@ EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_ve
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
            "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
            "lz4mi_frame_decompress", "lz4mi_frame_index", "lz4mi_compress_chain",
-           "lz4mi_host_compress_block", "lz4mi_host_compress_chain", "lz4mi_host_decompress_block")
+           "lz4mi_host_compress_block", "lz4mi_host_compress_chain", "lz4mi_host_decompress_block",
+           "lz4mi_copy_stored_blocks")
 
 
 class Lz4miError(RuntimeError):
@@ -108,6 +109,9 @@ def lib():
                                                   ctypes.c_uint64, ctypes.c_int64, _vp, ctypes.c_uint32, ctypes.c_uint32]
         L.lz4mi_frame_index.restype = ctypes.c_int32
         L.lz4mi_frame_index.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]
+        L.lz4mi_copy_stored_blocks.restype = ctypes.c_int32
+        L.lz4mi_copy_stored_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                               ctypes.c_uint32, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
         L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, _vp]
@@ -378,6 +382,13 @@ def frame_pack_dev(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, co
     _check(lib().lz4mi_frame_pack(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr,
                                   rec_off_ptr, nblocks, DEVICE_PTRS | (BLOCK_CHECKSUM if block_checksum else 0),
                                   stream or None))
+
+
+def copy_stored_blocks_dev(frame_ptr, frame_len, in_off_ptr, n_ptr, out_off_ptr, out_ptr, out_cap, nblocks, stream=0):
+    """Stored frame blocks into their output slots, one launch (include/lz4mi.h
+    lz4mi_copy_stored_blocks): device pointers, asynchronous on `stream`."""
+    _check(lib().lz4mi_copy_stored_blocks(frame_ptr, frame_len, in_off_ptr, n_ptr, out_off_ptr, out_ptr, out_cap,
+                                          nblocks, DEVICE_PTRS, stream or None))
 
 
 def frame_index_dev(frame_ptr, frame_len, pay_off_ptr, size_word_ptr, cap_blocks, info_ptr, stream=0):

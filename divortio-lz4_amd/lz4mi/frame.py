@@ -305,12 +305,36 @@ class ContentChecksum:
         return os.path.join(_shm_dir(), f"lz4mi_stage_{self.tag[0]}_{self.tag[1]}_{r}.bin{suffix}")
 
     def start(self, shard):
+        """Start the chain on `shard`. Work already queued on the caller's current stream that
+        writes `shard` is waited for (an event recorded here, waited on by the side stream), so
+        the caller need not synchronise first."""
         self.shard = shard
+        self.ready = None
+        self.cancel = False
         if self.route == "send":
             return self
+        if shard.device.type == "cuda":
+            import torch
+            self.ready = torch.cuda.Event()
+            self.ready.record(torch.cuda.current_stream(shard.device))
         self.thread = threading.Thread(target=self._run, daemon=True)
         self.thread.start()
         return self
+
+    def abort(self):
+        """Stop the chain after an error between start() and finish() (no collectives): the
+        thread ends at its next poll, and this call's staging files of this rank (all ranks'
+        on root) are removed."""
+        self.cancel = True
+        if getattr(self, "thread", None) is not None:
+            self.thread.join()
+        if self.route == "shm":
+            for r in (range(self.world) if self.rank == self.root else [self.rank]):
+                for suf in ("", ".done", ".err", ".done.tmp", ".err.tmp"):
+                    try:
+                        os.unlink(self._path(r, suf))
+                    except OSError:
+                        pass
 
     def _run(self):
         import time
@@ -319,6 +343,8 @@ class ContentChecksum:
         try:
             ctx = torch.cuda.device(self.shard.device) if self.shard.device.type == "cuda" else None
             side = torch.cuda.Stream(self.shard.device) if ctx is not None else None
+            if side is not None and self.ready is not None:
+                side.wait_event(self.ready)      # the shard's producers on the caller's stream
             if ctx is not None:
                 ctx.__enter__()
             try:
@@ -348,6 +374,8 @@ class ContentChecksum:
                         continue
                     deadline = time.perf_counter() + self.DEADLINE_S
                     while not os.path.exists(self._path(r, ".done")):
+                        if self.cancel:
+                            raise RuntimeError("lz4mi: content checksum aborted")
                         if os.path.exists(self._path(r, ".err")):
                             raise RuntimeError(f"lz4mi: rank {r} failed to stage its shard for the content checksum")
                         if time.perf_counter() > deadline:
@@ -463,13 +491,18 @@ def compress_frame_sharded(raw, block_size=4194304, content_checksum=True, add_c
     # the content checksum reads only the raw input: its chain starts now, beside the
     # kernel and the collective (bufferCompress.js:244-252 hashes the same bytes at the end)
     ck = ContentChecksum(n, dev, group, root).start(raw) if content_checksum else None
-    t0 = _phase(timings, "setup", t0, dev, group)
-    records = codec.records(raw, block_size, block_checksum)
-    if timings is not None and getattr(codec, "last_kernel_s", None) is not None:
-        timings["kernel_device"] = timings.get("kernel_device", 0.0) + codec.last_kernel_s
-    t0 = _phase(timings, "kernel", t0, dev, group)
-    body = shard.gather_records_to_root(records, root=root, group=group) if multi else records
-    t0 = _phase(timings, "collective", t0, dev, group)
+    try:
+        t0 = _phase(timings, "setup", t0, dev, group)
+        records = codec.records(raw, block_size, block_checksum)
+        if timings is not None and getattr(codec, "last_kernel_s", None) is not None:
+            timings["kernel_device"] = timings.get("kernel_device", 0.0) + codec.last_kernel_s
+        t0 = _phase(timings, "kernel", t0, dev, group)
+        body = shard.gather_records_to_root(records, root=root, group=group) if multi else records
+        t0 = _phase(timings, "collective", t0, dev, group)
+    except BaseException:
+        if ck is not None:
+            ck.abort()
+        raise
     csum = ck.finish() if ck is not None else None
     if timings is not None and ck is not None:
         timings["checksum_chain"] = timings.get("checksum_chain", 0.0) + ck.elapsed
@@ -567,32 +600,42 @@ class DeviceDecoder:
         status = torch.zeros(nb, dtype=torch.int32, device=dev)
         out_len = torch.zeros(nb, dtype=torch.int32, device=dev)
         ci = torch.nonzero(~stored).flatten()
-        if ci.numel():
-            c_in_off = pay_rel[ci].contiguous()
-            c_in_len = size[ci].to(torch.int32).contiguous()
-            c_out_off = slot_off[ci].contiguous()
-            c_cap = cap[ci].to(torch.int32).contiguous()
-            c_len = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
-            c_st = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(s):
-                e0.record(s)
+        si = torch.nonzero(stored).flatten()
+        # stored blocks larger than their slot: the reference's RangeError (result.set)
+        over = size[si] > cap[si]
+        if si.numel():
+            status[si[over]] = -8
+        si = si[~over]
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record(s)
+            if ci.numel():
+                c_in_off = pay_rel[ci].contiguous()
+                c_in_len = size[ci].to(torch.int32).contiguous()
+                c_out_off = slot_off[ci].contiguous()
+                c_cap = cap[ci].to(torch.int32).contiguous()
+                c_len = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
+                c_st = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
                 lz4mi.decompress_blocks_dev(rng.data_ptr(), c_in_off.data_ptr(), c_in_len.data_ptr(), out.data_ptr(),
                                             c_out_off.data_ptr(), c_cap.data_ptr(), c_len.data_ptr(), c_st.data_ptr(),
                                             ci.numel(), s.cuda_stream)
-                e1.record(s)
+            if si.numel():   # stored blocks: one launch (bufferDecompress.js:173-180), no per-block sync
+                s_in_off = pay_rel[si].contiguous()
+                s_len = size[si].to(torch.int32).contiguous()
+                s_out_off = slot_off[si].contiguous()
+                lz4mi.copy_stored_blocks_dev(rng.data_ptr(), rng.numel(), s_in_off.data_ptr(), s_len.data_ptr(),
+                                             s_out_off.data_ptr(), out.data_ptr(), out.numel(), si.numel(),
+                                             s.cuda_stream)
+            e1.record(s)
+            if ci.numel():
                 out_len[ci] = c_len
                 status[ci] = c_st
-            s.synchronize()
+            if si.numel():
+                out_len[si] = s_len
+        s.synchronize()
+        if ci.numel() or si.numel():
             self.last_kernel_s = e0.elapsed_time(e1) / 1e3
-        for b in torch.nonzero(stored).flatten().tolist():      # stored blocks (rare): plain copies
-            p, m = int(pay_rel[b]), int(size[b])
-            if m > int(cap[b]):
-                status[b] = -8                                  # the reference's RangeError (result.set)
-                continue
-            out[b * block_max:b * block_max + m].copy_(rng[p:p + m])
-            out_len[b] = m
         if nb == 0:
             return torch.zeros(0, dtype=torch.uint8, device=dev), status
         # every block but the last filled its slot (the reference encoder's layout): the slots
@@ -606,7 +649,7 @@ class DeviceDecoder:
 
 
 def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, decoder=None, gather=True,
-                             timings=None, device=None):
+                             timings=None, device=None, zero_copy=False):
     """Decode an independent-block frame with its blocks shared out over the ranks.
 
     frame: the whole frame on root (1-D uint8 tensor; a CUDA tensor is indexed and scattered
@@ -622,7 +665,9 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     plus kernel_device (the decoder's HIP-event time) and checksum_chain (the chain's own
     duration: it runs beside the gather, so checksum_wait is what it adds).
     `device`: where this rank's tensors live (default: frame's device on root, else the
-    backend's: CUDA for nccl, host for gloo)."""
+    backend's: CUDA for nccl, host for gloo). With a caller's `decoder` the un-gathered result
+    is a copy unless `zero_copy`: then it is a view of that decoder's workspace, overwritten
+    by the decoder's next call of the same shape (bench.py keeps one decoder and opts in)."""
     import time
     import torch
     import lz4mi
@@ -638,6 +683,7 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
     else:   # the backend's device: RCCL moves CUDA tensors, gloo host ones
         nccl = multi and dist.get_backend(group) == "nccl"
         dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    own_decoder = decoder is None
     decoder = decoder or DeviceDecoder()
     src = dist.get_global_rank(group, root) if (multi and group is not None) else root
     t0 = time.perf_counter()
@@ -734,7 +780,12 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
         ck = ContentChecksum(out.numel(), dev, group, root).start(out)
     got = None
     if gather and multi:
-        got = shard.gather_records_to_root(out, root=root, group=group)
+        try:
+            got = shard.gather_records_to_root(out, root=root, group=group)
+        except BaseException:
+            if ck is not None:
+                ck.abort()
+            raise
         t0 = _phase(timings, "gather", t0, dev, group)
     if ck is not None:
         d = ck.finish()
@@ -750,7 +801,12 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
         if not int(ok[0]):
             raise lz4mi.Lz4miError(lz4mi.ERR_CHECKSUM)
     if not gather or not multi:
-        return out if (rank == root or not gather) else None
+        if rank != root and gather:
+            return None
+        caller_ws = decoder is not None and getattr(decoder, "ws", None) is not None and \
+            out.numel() and out.data_ptr() >= decoder.ws[1].data_ptr() and \
+            out.data_ptr() < decoder.ws[1].data_ptr() + decoder.ws[1].numel()
+        return out.clone() if (caller_ws and not zero_copy and not own_decoder) else out
     return got
 
 

@@ -51,6 +51,8 @@ extern "C" {
 #define LZ4MI_ERR_HIP (-100)            /* a HIP runtime call failed */
 #define LZ4MI_ERR_ARG (-101)            /* invalid argument (size limits, NULL pointers) */
 #define LZ4MI_ERR_NO_DEVICE (-102)      /* no usable gfx950 device */
+#define LZ4MI_ERR_DEVICE_BOUND (-103)   /* lz4mi_init(d): the library is already bound to another device (one
+                                           device per process: its stream and scratch live on the first) */
 
 /* ---- flags --------------------------------------------------------------- */
 #define LZ4MI_DEVICE_PTRS 0x1u   /* all pointers are device pointers; async on `stream` */
@@ -256,6 +258,18 @@ int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_total, int64_
  */
 int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off, uint32_t* size_word,
                           uint32_t cap_blocks, int64_t* info, uint32_t flags, void* stream);
+
+/*
+ * Stored (uncompressed) frame blocks into their output slots, one launch for all of them:
+ * block b's n[b] bytes at frame + in_off[b] go to out + out_off[b] (clipped at the frame end
+ * and at out_cap). Replaces the stored branch of the reference's frame loop
+ * (src/buffer/bufferDecompress.js:173-180, result.set(input.subarray(...))); the caller
+ * checks each block against its slot first (the reference's RangeError). Device pointers
+ * only (LZ4MI_DEVICE_PTRS); asynchronous on `stream`.
+ */
+int32_t lz4mi_copy_stored_blocks(const uint8_t* frame, uint64_t len, const uint64_t* in_off, const uint32_t* n,
+                                 const uint64_t* out_off, uint8_t* out, uint64_t out_cap, uint32_t nblocks,
+                                 uint32_t flags, void* stream);
 
 /*
  * Synthetic input generator (bench/test support, not a reference interface):

@@ -42,6 +42,30 @@ def test_status_messages_are_the_reference_strings():
     assert lz4mi.status_message(-7) == "LZ4: Content Checksum Error"
 
 
+def test_one_device_per_process_status():
+    """a second device is refused with its own status, not a generic argument
+    error (the library's stream and scratch live on the first device it was bound to)."""
+    assert lz4mi.ERR_DEVICE_BOUND == -103
+    assert lz4mi.status_message(-103) == "lz4mi: library already bound to another device (one device per process)"
+
+
+def test_host_encoder_rejects_positions_past_int32():
+    """start + len past 2^31 would overflow the encoder's int32 positions
+    (the table holds position + 1); the host entry points refuse it before reading src."""
+    import ctypes
+    L = lz4mi.lib()
+    src = (ctypes.c_uint8 * 64)()
+    table = (ctypes.c_int32 * 16384)()
+    out = (ctypes.c_uint8 * 64)()
+    big = 1 << 32
+    r = L.lz4mi_host_compress_block(src, big, (1 << 31) - 10, 20, table, out, 64, 0)
+    assert r == lz4mi.ERR_ARG
+    offs = (ctypes.c_uint64 * 2)()
+    clen = (ctypes.c_uint32 * 2)()
+    r = L.lz4mi_host_compress_chain(src, big, (1 << 31) - 10, 20, 4 << 20, table, out, offs, clen)
+    assert r == lz4mi.ERR_ARG
+
+
 def test_host_xxh32_matches_reference(manifest):
     (c,) = cases_of(manifest, "xxh32")
     base = O.generate(c["input"]["gen"], c["input"]["seed"], c["input"]["n"])

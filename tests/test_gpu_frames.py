@@ -81,6 +81,78 @@ def test_config4_complete_frame_64mib():
     assert str(ei.value) == "LZ4: Content Checksum Error"
 
 
+def test_frame_checksum_waits_for_async_producer():
+    """compress_frame_sharded's content checksum starts on a side stream at
+    once; the shard written by work still queued on the caller's stream (here behind a
+    ~0.1 s device sleep, no synchronisation) must be hashed after that work, not before."""
+    from lz4mi import frame as F
+    n = 4
+    src = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    lz4mi.generate_blocks_dev(src.data_ptr(), "tiles216", 3, BLOCK, n, _stream())
+    torch.cuda.synchronize()
+    want = O.compress_frame(src.cpu().numpy(), None, BLOCK, True, True, True)
+    raw = torch.zeros(n * BLOCK, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)     # the producer is still queued when the call starts
+    raw.copy_(src)
+    got = F.compress_frame_sharded(raw, BLOCK, content_checksum=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want)
+
+
+def test_mostly_stored_frame_decodes_on_device():
+    """a 16-block frame of 12 random (stored) + 4 tiles216 blocks — the
+    GPU frame == the oracle's frame byte for byte, and the sharded device decode (stored blocks
+    copied by one lz4mi_copy_stored_blocks launch) returns the raw bytes; a stored block too
+    large for its slot reports the reference's RangeError."""
+    from lz4mi import frame as F
+    n = 16
+    kinds = ["random"] * 12 + ["tiles216"] * 4
+    order = [kinds[(5 * b) % n] for b in range(n)]          # interleaved
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+    for b, k in enumerate(order):
+        lz4mi.generate_blocks_dev(tmp.data_ptr(), k, 40 + b, BLOCK, 1, _stream())
+        raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+    torch.cuda.synchronize()
+    host = raw.cpu().numpy()
+    ref = O.compress_frame(host, None, BLOCK, True, True, True)
+    got = F.compress_frame_sharded(raw, BLOCK, content_checksum=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), ref)
+    meta, pay, word = F.frame_index(got)
+    assert int(((word & 0x80000000) != 0).sum()) == 12
+    dec = F.DeviceDecoder()
+    back = F.decompress_frame_sharded(got, verify_checksum=True, decoder=dec)
+    assert np.array_equal(back.cpu().numpy(), host)
+    assert dec.last_kernel_s is not None and dec.last_kernel_s > 0
+    # a stored block whose slot is too small: RangeError status (-8), nothing else touched
+    out, st = dec.decode(got, pay, word, BLOCK, BLOCK - 1)
+    last = n - 1
+    want = -8 if int(word[last]) & 0x80000000 else 0
+    assert int(st[last]) in (want, -1) and all(int(x) == 0 for x in st[:last].tolist())
+
+
+def test_decoder_workspace_aliasing():
+    """with a caller's DeviceDecoder the result is a copy (a later call of the same
+    shape does not overwrite it) unless zero_copy=True asks for the workspace view."""
+    from lz4mi import frame as F
+    n = 2
+    a = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    b = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    lz4mi.generate_blocks_dev(a.data_ptr(), "tiles216", 5, BLOCK, n, _stream())
+    lz4mi.generate_blocks_dev(b.data_ptr(), "tiles216", 9, BLOCK, n, _stream())
+    torch.cuda.synchronize()
+    fa = F.compress_frame_sharded(a, BLOCK)
+    fb = F.compress_frame_sharded(b, BLOCK)
+    dec = F.DeviceDecoder()
+    ra = F.decompress_frame_sharded(fa, decoder=dec)
+    rb = F.decompress_frame_sharded(fb, decoder=dec)
+    assert torch.equal(ra, a) and torch.equal(rb, b)
+    va = F.decompress_frame_sharded(fa, decoder=dec, zero_copy=True)
+    assert va.data_ptr() == dec.ws[1].data_ptr() and torch.equal(va, a)
+
+
 def test_config0_frame_through_device_path(manifest):
     """BASELINE configs[0], the reference benchmark's call (benchWorker.js:47-54,
     LZ4.compress(1 MiB of i % 251, null, 4194304, true, false)): the device frame path writes

@@ -26,11 +26,13 @@ def make_raw(torch, lz4mi, gen, n, sp):
     oracle's generators; per:<P> = P random bytes repeated; far = copies of 8-48 KiB
     windows from the previous 64 KiB, non-overlapping), 16 distinct blocks tiled."""
     raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
-    if gen == "mix":   # bench.py's 50/50 random/tiles216 mix (same shuffle)
+    if gen in ("mix", "mixc"):   # bench.py's 50/50 random/tiles216 mix (same shuffle), or clustered
         sys.path.insert(0, ROOT)
         from bench import mix_order
+        from lz4mi import shard
         tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
-        for b, kind in enumerate(mix_order(n)):
+        kinds = mix_order(n) if gen == "mix" else shard.clustered_mix_kinds(n)
+        for b, kind in enumerate(kinds):
             lz4mi.generate_blocks_dev(tmp.data_ptr(), kind, 1 + b, BLOCK, 1, sp)
             raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
     elif gen in lz4mi.GENERATORS:
