@@ -272,6 +272,93 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
     }
 
 
+def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 256, 2048, 4096), reps=3):
+    """device-resident kernel time (HIP events on the launch stream, median
+    of `reps`) of the first b blocks of the headline batch, decode and compress. One block is one
+    wave: below ~1 block per CU the time is one block's chain latency, above it the CUs' issue
+    and memory pipelines fill up."""
+    s = stream_obj.cuda_stream
+    res = {"blocks": [], "decompress_ms": [], "compress_ms": []}
+
+    def med(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream_obj)
+            fn()
+            e1.record(stream_obj)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return round(sorted(ts)[len(ts) // 2], 3)
+    scratch = torch.empty(batch.comp.numel(), dtype=torch.uint8, device="cuda")
+    slen = torch.zeros(batch.n, dtype=torch.int32, device="cuda")
+    for b in counts:
+        if b > batch.n:
+            continue
+        res["blocks"].append(b)
+        res["decompress_ms"].append(med(lambda: lz4mi.decompress_blocks_dev(
+            batch.comp.data_ptr(), batch.comp_off.data_ptr(), batch.comp_len.data_ptr(), batch.dec.data_ptr(),
+            batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), batch.dec_len.data_ptr(), batch.status.data_ptr(), b, s)))
+        res["compress_ms"].append(med(lambda: lz4mi.compress_blocks_dev(
+            batch.raw.data_ptr(), batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), scratch.data_ptr(),
+            batch.comp_off.data_ptr(), slen.data_ptr(), b, s)))
+    del scratch
+    torch.cuda.empty_cache()
+    res["note"] = "device-resident, HIP events; the first b blocks of the headline batch"
+    return res
+
+
+def mix_frame(torch, lz4mi, stream_obj, n):
+    """a frame of the 50/50 random/tiles216 mix (n blocks: the random ones are
+    stored blocks) decoded by DeviceDecoder (compressed blocks in one batch, stored ones in one
+    copy launch: `frame_kernel_ms` spans both) beside the batch decode of the same blocks
+    (every block an LZ4 block, one lz4mi_decompress_blocks launch)."""
+    from lz4mi import frame as F
+    s = stream_obj.cuda_stream
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+    for b, kind in enumerate(mix_order(n)):
+        lz4mi.generate_blocks_dev(tmp.data_ptr(), kind, 1 + b, BLOCK, 1, s)
+        raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+    del tmp
+    torch.cuda.synchronize()
+    codec = F.DeviceCodec(stream_obj)
+    dec = F.DeviceDecoder(stream_obj)
+    frame = F.compress_frame_sharded(raw, BLOCK, content_checksum=False, codec=codec)
+    meta, pay, word = F.frame_index(frame)
+    stored = int(((word & 0x80000000) != 0).sum().item())
+    ks = []
+    ok = True
+    for _ in range(4):
+        out = F.decompress_frame_sharded(frame, verify_checksum=False, decoder=dec, gather=False, zero_copy=True)
+        ks.append(dec.last_kernel_s * 1e3)
+    ok = bool(torch.equal(out, raw))
+    del out, frame, codec, dec
+    torch.cuda.empty_cache()
+    b2 = Batch.__new__(Batch)
+    b2.n, b2.raw = n, raw
+    b2.slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
+    b2.comp = torch.empty(n * b2.slot, dtype=torch.uint8, device="cuda")
+    b2.raw_off = torch.arange(n, dtype=torch.int64, device="cuda") * BLOCK
+    b2.raw_len = torch.full((n,), BLOCK, dtype=torch.int32, device="cuda")
+    b2.comp_off = torch.arange(n, dtype=torch.int64, device="cuda") * b2.slot
+    b2.comp_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    b2.dec = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    b2.dec_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    b2.status = torch.zeros(n, dtype=torch.int32, device="cuda")
+    b2.compress(lz4mi, s)
+    torch.cuda.synchronize()
+    _, kb = timed(torch, None, lambda: b2.decompress(lz4mi, s), 3, 1, stream_obj)
+    ok = ok and b2.verify(torch, lz4mi, s)
+    del b2, raw
+    torch.cuda.empty_cache()
+    fk = sorted(ks[1:])[1]
+    return {"blocks": n, "stored_blocks": stored, "frame_kernel_ms": round(fk, 3),
+            "batch_kernel_ms": round(kb * 1e3, 3), "frame_over_batch": round(fk / (kb * 1e3), 3), "verified": ok}
+
+
 def weak_scaling(torch, dist, walls, kern_s, bytes_per_rank, steps, device):
     """The bench's aggregation: every rank's timed-region wall times (`walls`, seconds) are
     max-reduced, value = all ranks' bytes / the slowest rank's wall (weak scaling: each rank
@@ -372,6 +459,9 @@ def reference_benchmark(with_js):
         return {"error": r.stderr[-500:]}
     out = {"workload": "LZ4.compress(x, null, 4194304, true, false) / LZ4.decompress of 25 MiB of one JSON record "
                        "repeated (the shape of the reference's benchmark data), host buffers through N-API; MB = 2^20 B",
+           "routes": "drop_in.auto: the default routing (7 blocks: below both crossovers, so the host codec; the "
+                     "*_route counts say which side each call took); drop_in.gpu: every block call forced onto the "
+                     "GPU kernels (LZ4.setRouting('gpu')) - the GPU's figure for this call size",
            "drop_in": json.loads(r.stdout.strip().splitlines()[-1]),
            "published_reference_MBps": {"compress_25MB": 484, "decompress_25MB": 459,
                                         "hardware": "MacBook Pro mid-2015 (i7 quad, Node 24), docs/BENCHMARKS.md"}}
@@ -490,6 +580,7 @@ def main():
                                                         args.steps, "cuda")
     ms_per_step = d_wall / args.steps * 1e3
 
+    lat = latency_curve(torch, lz4mi, batch, stream_obj) if args.extra and rank == 0 and world == 1 else None
     napi = napi_e2e(batch) if args.napi and rank == 0 and world == 1 else None
     single = single_block(torch, lz4mi, batch) if args.napi and rank == 0 and world == 1 else None
     c_base = c_cpu_baseline(batch, cpu_threads()) if args.cpu_baseline and rank == 0 and world == 1 else None
@@ -523,6 +614,11 @@ def main():
             frame = frame_workload(torch, dist, lz4mi, stream_obj, world, rank, args.frame_blocks)
         except Exception as e:    # reported, not fatal: every rank raises the same error (lz4mi.frame)
             frame = {"error": repr(e)[-500:]}
+        if world == 1 and args.extra:
+            try:
+                frame["mix_frame"] = mix_frame(torch, lz4mi, stream_obj, args.frame_blocks)
+            except Exception as e:
+                frame["mix_frame"] = {"error": repr(e)[-500:]}
     achieved = (raw_bytes + comp_bytes) / d_kern / 1e9
     traffic, traffic_src = pmc_traffic(lz4mi, n, args.gen)
     c_traffic, _ = pmc_traffic(lz4mi, n, args.gen, "pmc_traffic_compress.json")
@@ -566,6 +662,8 @@ def main():
         line["frame"] = frame
     if extra:
         line["variants"] = extra
+    if lat is not None:
+        line["latency_curve"] = lat
     if single is not None:
         line["single_block"] = single
     if napi is not None:

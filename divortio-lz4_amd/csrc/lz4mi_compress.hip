@@ -18,6 +18,12 @@
 
 #include <cstdlib>
 
+#ifndef LZ4MI_CPRIO
+#define LZ4MI_CPRIO 0   // batch encoder wave priority: 0 = chain 3, emission 0; 1 = by the share of the block
+                        // still to parse (thirds: chain 3/2/1, emission one below), so the youngest waves
+                        // of a SIMD (last in age arbitration) do not set the launch time (A/B switch)
+#endif
+
 #ifndef LZ4MI_CPROFILE
 #define LZ4MI_CPROFILE 0   // timing-only variant (tools/): per-phase wall-clock of the batch encoder
 #endif
@@ -59,6 +65,14 @@ struct CompArgs {
 };
 
 constexpr uint32_t kP1 = 2654435761u;
+
+// s_setprio with a run-time level 0..3 (the instruction takes an immediate)
+__device__ __forceinline__ void set_prio_lvl(uint32_t lvl) {
+    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 
 __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
@@ -684,9 +698,17 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         *(uint4*)&F.win[256 + 4 * lane] = r1;
         wb = b;
     };
+#if LZ4MI_CPRIO == 1
+    const int32_t t1 = n / 3, t2 = n - n / 3;
+#endif
     while (i < mflimit) {
         while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
+#if LZ4MI_CPRIO == 1
+        const uint32_t plvl = i < t1 ? 3u : i < t2 ? 2u : 1u;
+        set_prio_lvl(plvl);
+#else
         __builtin_amdgcn_s_setprio(3);
+#endif
         if (c == 67 && S > 0) {
             // ================= hit batch: probes at i + kS, k < K, each assumed a hit of step S
             int K;
@@ -736,9 +758,15 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
                 tcd = gt_code_of(F, h);
             }
             if (npend) {                                        // off the chain, while the reads are in flight
+#if LZ4MI_CPRIO == 1
+                set_prio_lvl(plvl - 1);
+                emit_batch(litv);
+                set_prio_lvl(plvl);
+#else
                 __builtin_amdgcn_s_setprio(0);
                 emit_batch(litv);
                 __builtin_amdgcn_s_setprio(3);
+#endif
             }
             // (the read's value is opaque until here: otherwise the compiler consumes it, and
             // waits for it, right after the load, before the emission)

@@ -56,12 +56,22 @@
 #ifndef LZ4MI_LL_SLEEP
 #define LZ4MI_LL_SLEEP 0   // long literal runs: s_sleep argument after every step (pacing A/B switch)
 #endif
+#ifndef LZ4MI_LL_ADAPT
+#define LZ4MI_LL_ADAPT 0   // long literal runs: s_sleep argument after every step while blocks with a
+                           // compression ratio above 2 run on the same XCD (adaptive pacing A/B switch)
+#endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
+#endif
+
+#ifndef LZ4MI_PRIO
+#define LZ4MI_PRIO 0   // wave priority: 0 = by phase (output 3 > walks 1 > table 0); 1 = by the share of
+                       // the block still to decode (more left: higher); 2 = by the wave's slot in its
+                       // SIMD (younger: higher); 3 = progress level + 1 in the output phase (A/B switch)
 #endif
 
 #ifndef LZ4MI_TIMELINE
@@ -73,6 +83,14 @@
 #endif
 
 namespace lz4mi {
+
+// s_setprio with a run-time level 0..3 (the instruction takes an immediate)
+__device__ __forceinline__ void set_prio(uint32_t lvl) {
+    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 
 // One 16-byte output piece (any alignment: gfx950 runs in unaligned mode), default cache
 // policy: the written lines stay in L2 for the history reads that follow (nontemporal
@@ -89,6 +107,15 @@ __device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
     const u32x4_nt t = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(t, (u32x4_nt*)p);
 }
+
+#if LZ4MI_LL_ADAPT
+__device__ unsigned int g_lat_active[8 * 32];   // per XCD (one 128-byte line each): latency-bound blocks running
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+#endif
 
 #if LZ4MI_TIMELINE
 constexpr uint32_t kTlMax = 16384;
@@ -920,6 +947,9 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
 // enough to keep HBM busy with one wave per block; the last piece overlaps its predecessor.
 __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, int32_t n, int lane) {
     constexpr int D = LZ4MI_LL_DEPTH;
+#if LZ4MI_LL_ADAPT
+    unsigned int* lat = &g_lat_active[32 * xcc_id()];
+#endif
     const int32_t np = (n + 15) >> 4;
     auto at = [&](int32_t p) { return 16 * p < n - 16 ? 16 * p : n - 16; };   // past the end: the last piece again
     for (int32_t p0 = lane; p0 < np; p0 += kWave * D) {
@@ -941,6 +971,11 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
         for (int j = 0; j < D; ++j) out16(dst + d[j], v[j]);
 #endif
         if (LZ4MI_LL_SLEEP) __builtin_amdgcn_s_sleep(LZ4MI_LL_SLEEP);
+#if LZ4MI_LL_ADAPT
+        // streaming beside latency-bound blocks: leave the CU's memory pipeline to them
+        if (__hip_atomic_load(lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+            __builtin_amdgcn_s_sleep(LZ4MI_LL_ADAPT);
+#endif
     }
 }
 
@@ -1147,6 +1182,20 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
+#if LZ4MI_PRIO == 1 || LZ4MI_PRIO == 3
+    const int32_t q1 = c.in_len / 4, q2 = c.in_len / 2, q3 = c.in_len - c.in_len / 4;   // progress levels
+#elif LZ4MI_PRIO == 2
+    {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        set_prio(hw & 3u);   // the wave's slot in its SIMD: later dispatched, higher
+    }
+#endif
+#if LZ4MI_LL_ADAPT
+    const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
+    unsigned int* lat = &g_lat_active[32 * xcc_id()];
+    if (lat_bound && lane == 0) atomicAdd(lat, 1u);
+#endif
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0;   // the next chunk's staged bytes, loaded early
     bool have_pf = false;
     int64_t pf_at = -1;                    // compressed position pf0/pf1 were loaded from
@@ -1186,7 +1235,13 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         // output rounds 3 > walks 1 > next-token table 0. The copies' loads and
         // stores go out first and the LDS-bound parse fills the gaps: tiles216 -0.9 %,
         // mix -2.5 %, copy -1.5 % (A/B in one process, profiles/r02j/prio_ab.json).
+#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(0);
+#elif LZ4MI_PRIO == 1 || LZ4MI_PRIO == 3
+        // VALU issue goes by priority, then age: with equal priorities the youngest waves of a
+        // SIMD finish last and set the launch time; the waves with the most left go first
+        set_prio(c.ip < q1 ? 3u : c.ip < q2 ? 2u : c.ip < q3 ? 1u : 0u);
+#endif
         // ---- 2. next-token table -----------------------------------------
         // Away from the block's end (fast_tab) four positions per lane from two stage
         // dwords, assuming length fields of at most one extension byte: a token whose
@@ -1226,7 +1281,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #endif
 
         PROF(1);
+#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(1);
+#endif
         // ---- 3. speculative walks + certification -------------------------
         uint32_t x;
         vis = 0;
@@ -1446,7 +1503,11 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
+#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(3);
+#elif LZ4MI_PRIO == 3
+        set_prio(c.ip < q2 ? 3u : c.ip < q3 ? 2u : 1u);
+#endif
         // ---- 5. output rounds ---------------------------------------------
         // The previous chunk's stores (read back as history below) and the next
         // chunk's loads are complete: the stores had the whole parse to drain.
@@ -1639,6 +1700,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         a.status[b] = status;
         a.out_len[b] = status ? 0u : (uint32_t)c.O;
     }
+#if LZ4MI_LL_ADAPT
+    if (lat_bound && lane == 0) atomicSub(lat, 1u);
+#endif
 #if LZ4MI_TIMELINE
     wait_vmem();
     const uint64_t tl_t1 = wall_clock64();

@@ -99,11 +99,29 @@ export function setRouting(mode) {
     routing = mode;
 }
 
+// Calls routed to each side since the last routeStats(true): what a figure measured through
+// this layer actually ran on (bench.py records them beside every drop-in rate).
+const routeCount = { host: 0, gpu: 0 };
+
 const hostRoute = (nblocks, max) => {
-    if (routing === 'gpu' || (routing === 'auto' && nblocks > max)) return false;
+    if (routing === 'gpu' || (routing === 'auto' && nblocks > max)) {
+        routeCount.gpu++;
+        return false;
+    }
+    // The host codec runs on this thread, yet it too requires the device: the drop-in is the
+    // GPU codec with a measured crossover, not a CPU library with a GPU option, so every route
+    // fails the same way without a gfx950 device (INTEGRATION.md, "Routing").
     requireDevice();
+    routeCount.host++;
     return true;
 };
+
+/** Calls routed to the host codec and to the GPU since the last reset: { host, gpu }. */
+export function routeStats(reset = false) {
+    const r = { host: routeCount.host, gpu: routeCount.gpu };
+    if (reset) routeCount.host = routeCount.gpu = 0;
+    return r;
+}
 
 /** compressBlock (src/block/blockCompress.js:31): one serial chain, the host encoder unless routing 'gpu'. */
 export function compressRaw(src, output, srcStart, srcLen, hashTable, outputOffset) {
@@ -281,6 +299,7 @@ export function compress(input, dictionary = null, maxBlockSize = 4194304, block
         // place — one serial chain, so the host route (the chain kernel runs it as one GPU
         // wave: 0.12 GB/s on tiles216 against ~1.5 GB/s for the host encoder, DESIGN §5).
         const nb = Math.ceil((end - pos) / bsize);
+        if (nb > 0) routeCount[routing === 'gpu' ? 'gpu' : 'host']++;
         if (nb > 0 && routing === 'gpu') {
             let slot = 0;
             const outOff = new Float64Array(nb), compLen = new Uint32Array(nb);
@@ -922,6 +941,7 @@ export const LZ4 = {
     LZ4Decoder,
     setDecodeMode,
     setRouting,
+    routeStats,
     version: native.version,
     buildId: native.buildId,
 };

@@ -29,25 +29,35 @@ const secs = (fn, n) => {               // median of n timed calls after a warm-
     return ts[(n - 1) >> 1];
 };
 const rate = (bytes, fn, n) => +(bytes / secs(fn, n) / 1e9).toFixed(3);
+// calls each side took during a measurement (warm-up included): which codec a rate describes
+const routed = (key, fn) => { LZ4.routeStats(true); fn(); out[`${key}_route`] = LZ4.routeStats(true); };
 const out = { bytes: input.length, routing: 'auto' };
 let frame = LZ4.compress(input, null, BS, true, false);
 out.ratio = +(input.length / frame.length).toFixed(3);
-out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, BS, true, false); }, reps);
+routed('compress_independent', () => {
+    out.compress_independent_GBps = rate(input.length, () => { frame = LZ4.compress(input, null, BS, true, false); }, reps);
+});
 const dep = input.subarray(0, depBytes);
 let depFrame = null;
-out.compress_dependent_default_GBps = rate(dep.length, () => { depFrame = LZ4.compress(dep); }, 1);
+routed('compress_dependent_default', () => {
+    out.compress_dependent_default_GBps = rate(dep.length, () => { depFrame = LZ4.compress(dep); }, 1);
+});
 out.dependent_bytes = dep.length;
 LZ4.setDecodeMode('spec');
 if (Buffer.compare(Buffer.from(LZ4.decompress(depFrame)), Buffer.from(dep)) !== 0)
     throw new Error('dependent frame round trip mismatch');
-out.decompress_dependent_GBps = rate(dep.length, () => LZ4.decompress(depFrame), 1);
+routed('decompress_dependent', () => {
+    out.decompress_dependent_GBps = rate(dep.length, () => LZ4.decompress(depFrame), 1);
+});
 for (const mode of ['spec', 'reference']) {
     LZ4.setDecodeMode(mode);
     const back = LZ4.decompress(frame);
     // (reference mode reproduces the reference decoder, which corrupts a few blocks: SURVEY F1)
     if (mode === 'spec' && Buffer.compare(Buffer.from(back), Buffer.from(input)) !== 0)
         throw new Error(`${mode} round trip mismatch`);
-    out[`decompress_${mode}_GBps`] = rate(input.length, () => LZ4.decompress(frame), reps);
+    routed(`decompress_${mode}`, () => {
+        out[`decompress_${mode}_GBps`] = rate(input.length, () => LZ4.decompress(frame), reps);
+    });
 }
 LZ4.setDecodeMode('spec');
 const cross = { block_bytes: BS, blocks: [], compress_ms: { gpu: [], host: [] }, decompress_ms: { gpu: [], host: [] } };
