@@ -24,7 +24,7 @@
 
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
-                                              int32_t*, uint32_t, int, hipStream_t);
+                                              int32_t*, uint32_t, int, uint32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
@@ -80,17 +80,19 @@ struct StreamCtx {
     Scratch tables;       // batch encoder hash tables (64 KiB per block)
     Scratch frame_meta;   // block-checksum payload offsets / lengths of frame_pack
     Scratch scan;         // frame_decompress: block lists of the device frame walk
+    Scratch order;        // batch decode: the blocks' dispatch order (lz4mi_block_order_kernel)
     void release() {
         tables.release();
         frame_meta.release();
         scan.release();
+        order.release();
     }
 };
 
 struct Ctx {
     std::atomic<int> device{-1};   // set once by init_locked, never changed after
     hipStream_t stream = nullptr;
-    Scratch in, out, meta, aux;   // staging of the synchronous host-pointer entry points
+    Scratch in, out, meta, aux, order;   // staging of the synchronous host-pointer entry points
     std::mutex mu;                // serialises the host-pointer entry points (their staging is shared)
     std::mutex streams_mu;
     std::vector<std::unique_ptr<StreamCtx>> streams;
@@ -142,11 +144,16 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
+// `order`: scratch of nblocks words for the dispatch order, owned by the caller's lock
+// (nullptr: the blocks go in index order)
 hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
-                         uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s) {
+                         uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
+                         Scratch* order) {
+    uint32_t* ord = nullptr;
+    if (order && nblocks > 1 && order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
-                                   nblocks, mode, s);
+                                   nblocks, mode, ord, s);
 }
 
 inline uint64_t round16(uint64_t n) { return (n + 15u) & ~15ull; }
@@ -332,8 +339,12 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
+        // the order scratch belongs to the stream: kernels of one stream use it in order
+        hipStream_t s = pick_stream(stream);
+        StreamCtx* c = stream_ctx(s);
+        std::lock_guard<std::mutex> sl(c->mu);
         LZ4MI_TRY(decode_launch(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
-                                mode, pick_stream(stream)));
+                                mode, s, &c->order));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_cap || !out_len || !status) return LZ4MI_ERR_ARG;
@@ -386,7 +397,8 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off, m_out_cap,
-                            dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks, mode, s));
+                            dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks, mode, s,
+                            &g_ctx.order));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
@@ -666,7 +678,7 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
     // stored blocks, then every compressed block in one batch (spec or reference-exact)
     LZ4MI_TRY(lz4mi_launch_frame_stored(frame, len, s_in_off, s_len, s_out_off, out, (uint64_t)hi[2], ns, s));
     if (nc) LZ4MI_TRY(decode_launch(frame, c_in_off, c_in_len, out, c_out_off, c_out_cap, nullptr, 0, d_out_len,
-                                    d_status, nc, mode, s));
+                                    d_status, nc, mode, s, &c->order));
     std::vector<uint32_t> olen(nc), cap(nc), cidx(nc), slen(ns), sidx(ns);
     std::vector<int32_t> stat(nc);
     std::vector<uint64_t> soff(ns), ooff(nc), ioff(nc);
@@ -688,7 +700,7 @@ int32_t lz4mi_frame_decompress(const uint8_t* frame, uint64_t len, uint8_t* out,
     for (uint32_t k = 0; k < nc; ++k) {
         if (stat[k] != LZ4MI_ERR_CROSS_BLOCK) continue;
         LZ4MI_TRY(decode_launch(frame, c_in_off + k, c_in_len + k, out, c_out_off + k, c_out_cap + k, nullptr, 0,
-                                d_out_len + k, d_status + k, 1, mode, s));
+                                d_out_len + k, d_status + k, 1, mode, s, nullptr));
         LZ4MI_TRY(hipMemcpyAsync(&olen[k], d_out_len + k, 4, hipMemcpyDeviceToHost, s));
         LZ4MI_TRY(hipMemcpyAsync(&stat[k], d_status + k, 4, hipMemcpyDeviceToHost, s));
         LZ4MI_TRY(hipStreamSynchronize(s));

@@ -19,6 +19,7 @@ struct DecArgs {
     uint32_t nblocks;
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
     int f1check;   // reference-exact (LZ4MI_JS_EXACT): fix up every chunk the reference's F1 rewrite changes
+    const uint32_t* order = nullptr;   // workgroup w decodes block order[w] (nullptr: block w)
 };
 
 }  // namespace lz4mi

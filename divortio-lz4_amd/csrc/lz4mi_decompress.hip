@@ -50,15 +50,13 @@
 #ifndef LZ4MI_LIT_NT
 #define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
 #endif
-#ifndef LZ4MI_LL_DEPTH
-#define LZ4MI_LL_DEPTH 4   // long literal runs: 16-byte pieces per lane in flight per step (A/B switch)
-#endif
-#ifndef LZ4MI_LL_SLEEP
-#define LZ4MI_LL_SLEEP 0   // long literal runs: s_sleep argument after every step (pacing A/B switch)
-#endif
 #ifndef LZ4MI_LL_ADAPT
-#define LZ4MI_LL_ADAPT 0   // long literal runs: s_sleep argument after every step while blocks with a
-                           // compression ratio above 2 run on the same XCD (adaptive pacing A/B switch)
+#define LZ4MI_LL_ADAPT 127   // long literal runs: s_sleep argument after every 4 KiB step while blocks with a
+                             // compression ratio above 2 run on the same XCD (0: no pacing; A/B switch)
+#endif
+#ifndef LZ4MI_ORDER
+#define LZ4MI_ORDER 1   // batches dispatched latency-bound blocks first, most compressed bytes first; 2: the
+                        // latency-bound blocks first in index order; 0: index order (A/B switch)
 #endif
 #ifndef LZ4MI_PER_ALIGN
 #define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
@@ -66,12 +64,6 @@
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
                          // 4 = output loads without stores, 5 = output stores without loads, 6 = round 1 only
-#endif
-
-#ifndef LZ4MI_PRIO
-#define LZ4MI_PRIO 0   // wave priority: 0 = by phase (output 3 > walks 1 > table 0); 1 = by the share of
-                       // the block still to decode (more left: higher); 2 = by the wave's slot in its
-                       // SIMD (younger: higher); 3 = progress level + 1 in the output phase (A/B switch)
 #endif
 
 #ifndef LZ4MI_TIMELINE
@@ -83,14 +75,6 @@
 #endif
 
 namespace lz4mi {
-
-// s_setprio with a run-time level 0..3 (the instruction takes an immediate)
-__device__ __forceinline__ void set_prio(uint32_t lvl) {
-    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
 
 // One 16-byte output piece (any alignment: gfx950 runs in unaligned mode), default cache
 // policy: the written lines stay in L2 for the history reads that follow (nontemporal
@@ -943,38 +927,49 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
 
 
 // A long literal run (incompressible data: one run per block) copied global ->
-// global with LZ4MI_LL_DEPTH 16-byte pieces per lane in flight (4 KiB per wave at 4),
-// enough to keep HBM busy with one wave per block; the last piece overlaps its predecessor.
+// global with 4 16-byte pieces per lane in flight (4 KiB per wave), enough to
+// keep HBM busy with one wave per block; the last piece overlaps its predecessor.
+// Paced (LZ4MI_LL_ADAPT) while latency-bound blocks run on the same XCD: at full rate
+// these copies fill the CU's vector-memory queues, and the blocks of short matches beside
+// them, whose every chunk waits on a few dependent history reads, slow down by ~25 % for
+// as long as the copies run (the per-block timeline, DESIGN §4.1 "Round 5"); spread out,
+// the copies finish later but inside those blocks' own lifetime.
 __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, int32_t n, int lane) {
-    constexpr int D = LZ4MI_LL_DEPTH;
-#if LZ4MI_LL_ADAPT
-    unsigned int* lat = &g_lat_active[32 * xcc_id()];
-#endif
     const int32_t np = (n + 15) >> 4;
     auto at = [&](int32_t p) { return 16 * p < n - 16 ? 16 * p : n - 16; };   // past the end: the last piece again
-    for (int32_t p0 = lane; p0 < np; p0 += kWave * D) {
-        int32_t d[D];
-        uint4 v[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) d[j] = at(p0 + j * kWave);
+#if LZ4MI_LL_ADAPT
+    const unsigned int* lat = &g_lat_active[32 * xcc_id()];
+#endif
+    for (int32_t p0 = lane; p0 < np; p0 += kWave * 4) {
+#if LZ4MI_LL_ADAPT
+        // (issued before the step's loads: its wait is not behind theirs)
+        const uint32_t busy = __hip_atomic_load(lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        const int32_t d0 = at(p0), d1 = at(p0 + kWave), d2 = at(p0 + 2 * kWave), d3 = at(p0 + 3 * kWave);
+        uint4 v0, v1, v2, v3;
 #if LZ4MI_LIT_NT
         // streamed once, never re-read soon: nontemporal, so they do not evict the history lines
         // other blocks' matches read back from L2
-#pragma unroll
-        for (int j = 0; j < D; ++j) v[j] = ld16_nt(src + d[j]);
-#pragma unroll
-        for (int j = 0; j < D; ++j) st16_nt(dst + d[j], v[j]);
+        v0 = ld16_nt(src + d0);
+        v1 = ld16_nt(src + d1);
+        v2 = ld16_nt(src + d2);
+        v3 = ld16_nt(src + d3);
+        st16_nt(dst + d0, v0);
+        st16_nt(dst + d1, v1);
+        st16_nt(dst + d2, v2);
+        st16_nt(dst + d3, v3);
 #else
-#pragma unroll
-        for (int j = 0; j < D; ++j) __builtin_memcpy(&v[j], src + d[j], 16);
-#pragma unroll
-        for (int j = 0; j < D; ++j) out16(dst + d[j], v[j]);
+        __builtin_memcpy(&v0, src + d0, 16);
+        __builtin_memcpy(&v1, src + d1, 16);
+        __builtin_memcpy(&v2, src + d2, 16);
+        __builtin_memcpy(&v3, src + d3, 16);
+        out16(dst + d0, v0);
+        out16(dst + d1, v1);
+        out16(dst + d2, v2);
+        out16(dst + d3, v3);
 #endif
-        if (LZ4MI_LL_SLEEP) __builtin_amdgcn_s_sleep(LZ4MI_LL_SLEEP);
 #if LZ4MI_LL_ADAPT
-        // streaming beside latency-bound blocks: leave the CU's memory pipeline to them
-        if (__hip_atomic_load(lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-            __builtin_amdgcn_s_sleep(LZ4MI_LL_ADAPT);
+        if (busy) __builtin_amdgcn_s_sleep(LZ4MI_LL_ADAPT);
 #endif
     }
 }
@@ -1160,8 +1155,8 @@ __device__ void f1_fixup(const Ctx c, const DecShared& S, int lane, uint32_t nse
 __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     __shared__ DecShared S;
     const int lane = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    if (b >= a.nblocks) return;
+    if (blockIdx.x >= a.nblocks) return;
+    const uint32_t b = a.order ? uniform(a.order[blockIdx.x]) : blockIdx.x;
 #if LZ4MI_TIMELINE
     const uint64_t tl_t0 = wall_clock64();
 #endif
@@ -1182,15 +1177,6 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
-#if LZ4MI_PRIO == 1 || LZ4MI_PRIO == 3
-    const int32_t q1 = c.in_len / 4, q2 = c.in_len / 2, q3 = c.in_len - c.in_len / 4;   // progress levels
-#elif LZ4MI_PRIO == 2
-    {
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        set_prio(hw & 3u);   // the wave's slot in its SIMD: later dispatched, higher
-    }
-#endif
 #if LZ4MI_LL_ADAPT
     const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
     unsigned int* lat = &g_lat_active[32 * xcc_id()];
@@ -1235,13 +1221,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         // output rounds 3 > walks 1 > next-token table 0. The copies' loads and
         // stores go out first and the LDS-bound parse fills the gaps: tiles216 -0.9 %,
         // mix -2.5 %, copy -1.5 % (A/B in one process, profiles/r02j/prio_ab.json).
-#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(0);
-#elif LZ4MI_PRIO == 1 || LZ4MI_PRIO == 3
-        // VALU issue goes by priority, then age: with equal priorities the youngest waves of a
-        // SIMD finish last and set the launch time; the waves with the most left go first
-        set_prio(c.ip < q1 ? 3u : c.ip < q2 ? 2u : c.ip < q3 ? 1u : 0u);
-#endif
         // ---- 2. next-token table -----------------------------------------
         // Away from the block's end (fast_tab) four positions per lane from two stage
         // dwords, assuming length fields of at most one extension byte: a token whose
@@ -1281,9 +1261,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #endif
 
         PROF(1);
-#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(1);
-#endif
         // ---- 3. speculative walks + certification -------------------------
         uint32_t x;
         vis = 0;
@@ -1503,11 +1481,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         PROF(4);
-#if LZ4MI_PRIO == 0
         __builtin_amdgcn_s_setprio(3);
-#elif LZ4MI_PRIO == 3
-        set_prio(c.ip < q2 ? 3u : c.ip < q3 ? 2u : 1u);
-#endif
         // ---- 5. output rounds ---------------------------------------------
         // The previous chunk's stores (read back as history below) and the next
         // chunk's loads are complete: the stores had the whole parse to drain.
@@ -1720,6 +1694,54 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block(a); }
 
+// Dispatch order of a batch (LZ4MI_ORDER). Every block is one wave and a batch of up to
+// 16 blocks per CU is resident at once, so a block's decode time is its chain latency under
+// the contention of the waves beside it; and workgroups land on CUs by index (round-robin
+// over the XCDs and their CUs: w, w + 256, ... share a CU, observed, used for speed only), in
+// age order within a SIMD, whose oldest wave wins VALU arbitration. Measured per block
+// (tools/timeline.py): tiles216 blocks in the youngest wave slot take 7 % longer than in the
+// oldest, and blocks with more compressed bytes longer still, so the launch ends with the
+// young heavy blocks; in the 50/50 random/tiles216 mix, CUs that drew more tiles216 blocks
+// finish last. The order: blocks with a compression ratio above 2 (latency-bound chains of
+// short matches) first, most compressed bytes first, then the rest in index order -- the
+// heavy blocks get the oldest slots and every CU the same share of chains. A stable key
+// sort (LDS bitonic) in one workgroup; batches of more than kOrderMax blocks keep their order.
+constexpr uint32_t kOrderMax = 8192;
+__global__ __launch_bounds__(1024) void lz4mi_block_order_kernel(const uint32_t* in_len, const uint32_t* out_cap,
+                                                                 uint32_t n, uint32_t* order) {
+    __shared__ uint64_t key[kOrderMax];
+    const uint32_t t = threadIdx.x;
+    uint32_t m = 2;
+    while (m < n) m <<= 1;
+    for (uint32_t i = t; i < m; i += 1024) {
+        uint64_t k = ~0ull;
+        if (i < n) {
+            const uint32_t il = in_len[i], oc = out_cap[i];
+            const bool lat = (uint64_t)il * 2 < (uint64_t)oc;
+            const uint32_t work = LZ4MI_ORDER == 2 ? 0u : (il > 0x7FFFFFFFu ? 0x7FFFFFFFu : il);   // 2: classes only
+            const uint32_t hi = lat ? 0x7FFFFFFFu - work : 0x80000000u;
+            k = ((uint64_t)hi << 32) | i;
+        }
+        key[i] = k;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= m; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t i = t; i < (m >> 1); i += 1024) {
+                const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const uint64_t x = key[lo], y = key[hi];
+                if ((x > y) == asc) {
+                    key[lo] = y;
+                    key[hi] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = t; i < n; i += 1024) order[i] = (uint32_t)key[i];
+}
+
 }  // namespace lz4mi
 
 #if LZ4MI_PROFILE
@@ -1743,13 +1765,20 @@ extern "C" int lz4mi_debug_timeline(unsigned long long* t, unsigned int* id, uns
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                               uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                               const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
-                                              int32_t* status, uint32_t nblocks, int mode, hipStream_t stream) {
+                                              int32_t* status, uint32_t nblocks, int mode, uint32_t* order,
+                                              hipStream_t stream) {
     // mode 0: LZ4 spec; 1: reference-exact serial kernel; 2: spec kernel with the in-chunk
-    // reference-exact fix-up of every chunk a double-copy-tail rewrite changes (f1_fixup)
+    // reference-exact fix-up of every chunk a double-copy-tail rewrite changes (f1_fixup).
+    // order: nblocks words of scratch for the dispatch order (nullptr: index order)
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, mode == 2 ? 1 : 0};
     if (nblocks == 0) return hipSuccess;
     if (mode == 1) return lz4mi_launch_decompress_serial(a, stream);
+    if (LZ4MI_ORDER && order && nblocks > 1 && nblocks <= lz4mi::kOrderMax) {
+        hipLaunchKernelGGL(lz4mi::lz4mi_block_order_kernel, dim3(1), dim3(1024), 0, stream, in_len, out_cap, nblocks,
+                           order);
+        a.order = order;
+    }
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
