@@ -18,10 +18,8 @@
 
 #include <cstdlib>
 
-#ifndef LZ4MI_CPRIO
-#define LZ4MI_CPRIO 0   // batch encoder wave priority: 0 = chain 3, emission 0; 1 = by the share of the block
-                        // still to parse (thirds: chain 3/2/1, emission one below), so the youngest waves
-                        // of a SIMD (last in age arbitration) do not set the launch time (A/B switch)
+#ifndef LZ4MI_CTIMELINE
+#define LZ4MI_CTIMELINE 0   // diagnostic build (tools/timeline.py --what compress): per-block start / end, HW_ID
 #endif
 
 #ifndef LZ4MI_CPROFILE
@@ -66,13 +64,6 @@ struct CompArgs {
 
 constexpr uint32_t kP1 = 2654435761u;
 
-// s_setprio with a run-time level 0..3 (the instruction takes an immediate)
-__device__ __forceinline__ void set_prio_lvl(uint32_t lvl) {
-    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-}
 
 __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
@@ -698,17 +689,9 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         *(uint4*)&F.win[256 + 4 * lane] = r1;
         wb = b;
     };
-#if LZ4MI_CPRIO == 1
-    const int32_t t1 = n / 3, t2 = n - n / 3;
-#endif
     while (i < mflimit) {
         while ((i >> 15) > g) gt_scrub_epoch(F, lane, ++g);
-#if LZ4MI_CPRIO == 1
-        const uint32_t plvl = i < t1 ? 3u : i < t2 ? 2u : 1u;
-        set_prio_lvl(plvl);
-#else
         __builtin_amdgcn_s_setprio(3);
-#endif
         if (c == 67 && S > 0) {
             // ================= hit batch: probes at i + kS, k < K, each assumed a hit of step S
             int K;
@@ -758,15 +741,9 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
                 tcd = gt_code_of(F, h);
             }
             if (npend) {                                        // off the chain, while the reads are in flight
-#if LZ4MI_CPRIO == 1
-                set_prio_lvl(plvl - 1);
-                emit_batch(litv);
-                set_prio_lvl(plvl);
-#else
                 __builtin_amdgcn_s_setprio(0);
                 emit_batch(litv);
                 __builtin_amdgcn_s_setprio(3);
-#endif
             }
             // (the read's value is opaque until here: otherwise the compiler consumes it, and
             // waits for it, right after the load, before the emission)
@@ -914,10 +891,19 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     return o.op;
 }
 
+#if LZ4MI_CTIMELINE
+constexpr uint32_t kCtlMax = 16384;
+__device__ unsigned long long g_ctl[2 * kCtlMax];   // per block: start, end (s_memrealtime, 100 MHz)
+__device__ unsigned int g_ctl_id[2 * kCtlMax];      // per block: HW_ID, XCC_ID
+#endif
+
 __global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, int32_t* tables) {
     __shared__ GtsShared F;
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
+#if LZ4MI_CTIMELINE
+    const uint64_t tl_t0 = wall_clock64();
+#endif
     CompJob j;
     j.src = a.in + a.in_off[b];
     j.src_total = a.in_len[b];
@@ -929,6 +915,19 @@ __global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, i
     j.table = nullptr;
     const int64_t r = compress_block_gts(j, F, tables + (size_t)b * 16384, threadIdx.x);
     if (threadIdx.x == 0) a.out_len[b] = (uint32_t)r;
+#if LZ4MI_CTIMELINE
+    wait_vmem();
+    const uint64_t tl_t1 = wall_clock64();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (threadIdx.x == 0 && b < kCtlMax) {
+        g_ctl[2 * b] = tl_t0;
+        g_ctl[2 * b + 1] = tl_t1;
+        g_ctl_id[2 * b] = hw;
+        g_ctl_id[2 * b + 1] = xcc;
+    }
+#endif
 }
 
 
@@ -1210,6 +1209,15 @@ __global__ __launch_bounds__(64) void lz4mi_compress_chain_kernel(ChainArgs a) {
 }
 
 }  // namespace lz4mi
+
+#if LZ4MI_CTIMELINE
+// The last batch-encoder launch's per-block timeline (as lz4mi_debug_timeline for the decoder).
+extern "C" int lz4mi_debug_ctimeline(unsigned long long* t, unsigned int* id, unsigned int n) {
+    if (n > lz4mi::kCtlMax) n = lz4mi::kCtlMax;
+    if (hipMemcpyFromSymbol(t, HIP_SYMBOL(lz4mi::g_ctl), sizeof(unsigned long long) * 2 * n) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(id, HIP_SYMBOL(lz4mi::g_ctl_id), sizeof(unsigned int) * 2 * n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if LZ4MI_CPROFILE
 extern "C" int lz4mi_debug_cprof(unsigned long long* out) {

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--gens", default="mix,mixc,tiles216")
     ap.add_argument("--blocks", type=int, default=4096)
     ap.add_argument("--out", default="gpurun_out/tl")
+    ap.add_argument("--what", default="decompress", help="decompress, or compress (a -DLZ4MI_CTIMELINE=1 build)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -44,8 +45,11 @@ def main():
     L.lz4mi_decompress_blocks.argtypes = lz4mi.lib().lz4mi_decompress_blocks.argtypes
     L.lz4mi_init.restype = ctypes.c_int32
     assert L.lz4mi_init(0) == 0
-    L.lz4mi_debug_timeline.restype = ctypes.c_int
-    L.lz4mi_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    dbg = L.lz4mi_debug_ctimeline if args.what == "compress" else L.lz4mi_debug_timeline
+    dbg.restype = ctypes.c_int
+    dbg.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    L.lz4mi_compress_blocks.restype = ctypes.c_int32
+    L.lz4mi_compress_blocks.argtypes = lz4mi.lib().lz4mi_compress_blocks.argtypes
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
     sp = s.cuda_stream
@@ -57,9 +61,13 @@ def main():
         torch.cuda.synchronize()
 
         def run():
-            r = L.lz4mi_decompress_blocks(B.comp.data_ptr(), B.comp_off.data_ptr(), B.comp_len.data_ptr(),
-                                          B.dec.data_ptr(), B.raw_off.data_ptr(), B.raw_len.data_ptr(), None, 0,
-                                          B.dec_len.data_ptr(), B.status.data_ptr(), n, 1, sp)
+            if args.what == "compress":
+                r = L.lz4mi_compress_blocks(B.raw.data_ptr(), B.raw_off.data_ptr(), B.raw_len.data_ptr(),
+                                            B.comp.data_ptr(), B.comp_off.data_ptr(), B.comp_len.data_ptr(), n, 1, sp)
+            else:
+                r = L.lz4mi_decompress_blocks(B.comp.data_ptr(), B.comp_off.data_ptr(), B.comp_len.data_ptr(),
+                                              B.dec.data_ptr(), B.raw_off.data_ptr(), B.raw_len.data_ptr(), None, 0,
+                                              B.dec_len.data_ptr(), B.status.data_ptr(), n, 1, sp)
             assert r == 0
         for _ in range(3):
             run()
@@ -70,10 +78,13 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         kms = e0.elapsed_time(e1)
+        if args.what == "compress":
+            B.decompress(lz4mi, sp)
+            torch.cuda.synchronize()
         ok = bool(torch.equal(B.dec, B.raw)) and bool((B.status == 0).all())
         t = np.zeros(2 * n, dtype=np.uint64)
         ids = np.zeros(2 * n, dtype=np.uint32)
-        assert L.lz4mi_debug_timeline(t.ctypes.data, ids.ctypes.data, n) == 0
+        assert dbg(t.ctypes.data, ids.ctypes.data, n) == 0
         clen = B.comp_len.cpu().numpy().astype(np.int64)
         t0 = t[0::2].astype(np.int64)
         t1 = t[1::2].astype(np.int64)
@@ -85,7 +96,9 @@ def main():
         keys = [cu_key(ids[2 * b], ids[2 * b + 1]) for b in range(n)]
         cus = sorted(set(keys))
         cu_of = np.array([cus.index(k) for k in keys])
-        np.savez(os.path.join(args.out, f"timeline_{gen}.npz"), start=start, end=end, clen=clen, cu=cu_of,
+        wave = ids[0::2] & 15
+        res_slot = [round(float(dur[wave == x].mean()), 3) if (wave == x).any() else None for x in range(4)]
+        np.savez(os.path.join(args.out, f"timeline_{args.what}_{gen}.npz"), start=start, end=end, clen=clen, cu=cu_of,
                  hw=ids[0::2], xcc=ids[1::2])
 
         def st(x):
@@ -95,6 +108,7 @@ def main():
             return {"n": int(len(x)), "mean": round(float(x.mean()), 3),
                     "min/p10/p50/p90/max": [round(float(v), 3) for v in q]}
         res = {"kernel_ms": round(kms, 3), "ok": ok, "span_ms": round(float(end.max()), 3), "cus": len(cus),
+               "dur_by_wave_slot_ms": res_slot,
                "blocks_per_cu": st(np.bincount(cu_of).astype(float)),
                "start_ms": st(start), "tiles_dur_ms": st(dur[~rnd]), "random_dur_ms": st(dur[rnd]),
                "tiles_end_ms": st(end[~rnd]), "random_end_ms": st(end[rnd])}
@@ -111,11 +125,11 @@ def main():
             res["running_random"] = [int(((start <= m) & (end > m) & rnd).sum()) for m in mid]
             res["running_tiles"] = [int(((start <= m) & (end > m) & ~rnd).sum()) for m in mid]
             res["bin_ms"] = round(float(edges[1]), 3)
-        summary[gen] = res
+        summary[f"{args.what}/{gen}"] = res
         print(gen, json.dumps(res), flush=True)
         del B
         torch.cuda.empty_cache()
-    with open(os.path.join(args.out, "timeline_summary.json"), "w") as f:
+    with open(os.path.join(args.out, f"timeline_summary_{args.what}.json"), "w") as f:
         json.dump(summary, f, indent=1)
 
 
