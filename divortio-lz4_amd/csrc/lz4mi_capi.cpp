@@ -336,7 +336,11 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     DeviceGuard dg;
     if (dg.status()) return dg.status();
     const int js = (flags & LZ4MI_JS_COMPAT) ? 1 : 0;
-    const int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
+    int mode = js ? 1 : ((flags & LZ4MI_JS_EXACT) ? 2 : 0);
+    if (flags & LZ4MI_FRAME_WORDS) {   // frame size words (stored bit): the batch kernel, device pointers
+        if (js || !(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
+        mode |= 4;
+    }
     if (nblocks == 0) return LZ4MI_OK;
     if (flags & LZ4MI_DEVICE_PTRS) {
         // the order scratch belongs to the stream: kernels of one stream use it in order
@@ -735,18 +739,6 @@ int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off,
     if (!(flags & LZ4MI_DEVICE_PTRS) || !frame || !info || (cap_blocks && (!pay_off || !size_word)))
         return LZ4MI_ERR_ARG;
     LZ4MI_TRY(lz4mi_launch_frame_index(frame, len, cap_blocks, pay_off, size_word, info, pick_stream(stream)));
-    return LZ4MI_OK;
-}
-
-int32_t lz4mi_copy_stored_blocks(const uint8_t* frame, uint64_t len, const uint64_t* in_off, const uint32_t* n,
-                                 const uint64_t* out_off, uint8_t* out, uint64_t out_cap, uint32_t nblocks,
-                                 uint32_t flags, void* stream) {
-    DeviceGuard dg;
-    if (dg.status()) return dg.status();
-    if (!(flags & LZ4MI_DEVICE_PTRS)) return LZ4MI_ERR_ARG;
-    if (nblocks == 0) return LZ4MI_OK;
-    if (!frame || !in_off || !n || !out_off || !out) return LZ4MI_ERR_ARG;
-    LZ4MI_TRY(lz4mi_launch_frame_stored(frame, len, in_off, n, out_off, out, out_cap, nblocks, pick_stream(stream)));
     return LZ4MI_OK;
 }
 

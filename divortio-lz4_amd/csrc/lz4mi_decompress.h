@@ -20,6 +20,7 @@ struct DecArgs {
     int isolate;   // batched blocks: a back-reference before the block start is reported, not followed
     int f1check;   // reference-exact (LZ4MI_JS_EXACT): fix up every chunk the reference's F1 rewrite changes
     const uint32_t* order = nullptr;   // workgroup w decodes block order[w] (nullptr: block w)
+    int frame_words = 0;               // in_len[b] is a frame size word: bit 31 = stored block (copied)
 };
 
 }  // namespace lz4mi

@@ -127,7 +127,8 @@ constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular 
 constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
 constexpr int kMaxSeq = kChunk / 3 + 3;       // tokens starting in the chunk: every non-final sequence is >= 3 bytes
 constexpr uint32_t kWarm = 512;               // speculative walks start this far before their segment
-constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
+constexpr int kMaxVarint = 250;
+constexpr int32_t LZ4MI_ERR_RANGE_STATUS = -8;   // include/lz4mi.h LZ4MI_ERR_RANGE               // longer length varints go to the cut path (ml < 65536)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
 constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
@@ -1167,7 +1168,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const uint32_t out_cap = uniform(a.out_cap[b]);
     Ctx c;
     c.blk = a.in + in_off;
-    c.in_len = (int32_t)uniform(a.in_len[b]);
+    const uint32_t word = uniform(a.in_len[b]);
+    c.in_len = (int32_t)(a.frame_words ? word & 0x7FFFFFFFu : word);
     c.out_off = (int64_t)out_off;
     c.dst = a.out + out_off;
     c.cap = out_cap > 0x7FFFFFFFu ? 0x7FFFFFFF : (int32_t)out_cap;
@@ -1177,6 +1179,23 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     c.ip = 0;
     c.O = 0;
     int32_t status = 0;
+    if (a.frame_words && (word & 0x80000000u)) {
+        // a frame's stored block (bufferDecompress.js:173-180): its bytes, in this launch, paced
+        // like any long literal run; larger than the slot: the reference's RangeError
+        const int32_t n = c.in_len;
+        if ((uint32_t)n > out_cap) {
+            status = LZ4MI_ERR_RANGE_STATUS;
+        } else if (n >= 16) {
+            long_literals(c.dst, c.blk, n, lane);
+        } else if (lane < n) {
+            c.dst[lane] = c.blk[lane];
+        }
+        if (lane == 0) {
+            a.status[b] = status;
+            a.out_len[b] = status ? 0u : (uint32_t)n;
+        }
+        return;
+    }
 #if LZ4MI_LL_ADAPT
     const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
     unsigned int* lat = &g_lat_active[32 * xcc_id()];
@@ -1716,7 +1735,7 @@ __global__ __launch_bounds__(1024) void lz4mi_block_order_kernel(const uint32_t*
     for (uint32_t i = t; i < m; i += 1024) {
         uint64_t k = ~0ull;
         if (i < n) {
-            const uint32_t il = in_len[i], oc = out_cap[i];
+            const uint32_t il = in_len[i], oc = out_cap[i];   // (a stored frame block: bit 31, not latency-bound)
             const bool lat = (uint64_t)il * 2 < (uint64_t)oc;
             const uint32_t work = LZ4MI_ORDER == 2 ? 0u : (il > 0x7FFFFFFFu ? 0x7FFFFFFFu : il);   // 2: classes only
             const uint32_t hi = lat ? 0x7FFFFFFFu - work : 0x80000000u;
@@ -1770,8 +1789,12 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
     // mode 0: LZ4 spec; 1: reference-exact serial kernel; 2: spec kernel with the in-chunk
     // reference-exact fix-up of every chunk a double-copy-tail rewrite changes (f1_fixup).
     // order: nblocks words of scratch for the dispatch order (nullptr: index order)
+    // mode bit 2 (4): in_len holds frame size words (LZ4MI_FRAME_WORDS)
+    const int fw = (mode & 4) ? 1 : 0;
+    mode &= 3;
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, mode == 2 ? 1 : 0};
+    a.frame_words = fw;
     if (nblocks == 0) return hipSuccess;
     if (mode == 1) return lz4mi_launch_decompress_serial(a, stream);
     if (LZ4MI_ORDER && order && nblocks > 1 && nblocks <= lz4mi::kOrderMax) {

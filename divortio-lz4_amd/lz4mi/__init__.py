@@ -29,6 +29,7 @@ JS_EXACT = 0x8
 XXH_STANDARD = 0x4
 XXH_LEN64 = 0x10
 BLOCK_CHECKSUM = 0x20
+FRAME_WORDS = 0x40
 
 GEN_RANDOM, GEN_REPETITIVE, GEN_TILES216 = 0, 1, 2
 GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GEN_TILES216}
@@ -39,8 +40,7 @@ EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_ve
            "lz4mi_xxh32", "lz4mi_xxh32_blocks", "lz4mi_frame_pack", "lz4mi_generate_blocks",
            "lz4mi_build_id", "lz4mi_xxh32_reset", "lz4mi_xxh32_update", "lz4mi_xxh32_digest",
            "lz4mi_frame_decompress", "lz4mi_frame_index", "lz4mi_compress_chain",
-           "lz4mi_host_compress_block", "lz4mi_host_compress_chain", "lz4mi_host_decompress_block",
-           "lz4mi_copy_stored_blocks")
+           "lz4mi_host_compress_block", "lz4mi_host_compress_chain", "lz4mi_host_decompress_block")
 
 
 class Lz4miError(RuntimeError):
@@ -109,9 +109,6 @@ def lib():
                                                   ctypes.c_uint64, ctypes.c_int64, _vp, ctypes.c_uint32, ctypes.c_uint32]
         L.lz4mi_frame_index.restype = ctypes.c_int32
         L.lz4mi_frame_index.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]
-        L.lz4mi_copy_stored_blocks.restype = ctypes.c_int32
-        L.lz4mi_copy_stored_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint64,
-                                               ctypes.c_uint32, ctypes.c_uint32, _vp]
         L.lz4mi_generate_blocks.restype = ctypes.c_int32
         L.lz4mi_generate_blocks.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, _vp]
@@ -344,10 +341,14 @@ def xxh32_blocks(blocks, seed=0, standard=False):
 # Raw device pointers (ints, e.g. torch tensor .data_ptr()) and a hipStream_t
 # handle (int, e.g. torch.cuda.current_stream().cuda_stream). Async.
 def decompress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr, out_len_ptr,
-                          status_ptr, nblocks, stream=0, js_compat=False, dict_ptr=None, dict_len=0):
+                          status_ptr, nblocks, stream=0, js_compat=False, dict_ptr=None, dict_len=0,
+                          frame_words=False):
+    """Batch decode on device pointers. frame_words: in_len holds frame size words (bit 31 =
+    stored block, copied in the same launch; include/lz4mi.h LZ4MI_FRAME_WORDS)."""
     _check(lib().lz4mi_decompress_blocks(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr,
                                          dict_ptr, dict_len, out_len_ptr, status_ptr, nblocks,
-                                         DEVICE_PTRS | (JS_COMPAT if js_compat else 0), stream or None))
+                                         DEVICE_PTRS | (JS_COMPAT if js_compat else 0) |
+                                         (FRAME_WORDS if frame_words else 0), stream or None))
 
 
 def compress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_len_ptr, nblocks, stream=0):
@@ -382,13 +383,6 @@ def frame_pack_dev(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, co
     _check(lib().lz4mi_frame_pack(raw_ptr, raw_off_ptr, raw_len_ptr, comp_ptr, comp_off_ptr, comp_len_ptr, frame_ptr,
                                   rec_off_ptr, nblocks, DEVICE_PTRS | (BLOCK_CHECKSUM if block_checksum else 0),
                                   stream or None))
-
-
-def copy_stored_blocks_dev(frame_ptr, frame_len, in_off_ptr, n_ptr, out_off_ptr, out_ptr, out_cap, nblocks, stream=0):
-    """Stored frame blocks into their output slots, one launch (include/lz4mi.h
-    lz4mi_copy_stored_blocks): device pointers, asynchronous on `stream`."""
-    _check(lib().lz4mi_copy_stored_blocks(frame_ptr, frame_len, in_off_ptr, n_ptr, out_off_ptr, out_ptr, out_cap,
-                                          nblocks, DEVICE_PTRS, stream or None))
 
 
 def frame_index_dev(frame_ptr, frame_len, pay_off_ptr, size_word_ptr, cap_blocks, info_ptr, stream=0):

@@ -586,8 +586,6 @@ class DeviceDecoder:
         nb = pay_rel.numel()
         s = self.stream if self.stream is not None else torch.cuda.current_stream(dev)
         self.last_kernel_s = None
-        size = word & 0x7FFFFFFF
-        stored = (word & 0x80000000) != 0
         cap = torch.full((nb,), block_max, dtype=torch.int64, device=dev)
         if nb:
             cap[-1] = last_cap
@@ -599,42 +597,23 @@ class DeviceDecoder:
         out = self.ws[1]
         status = torch.zeros(nb, dtype=torch.int32, device=dev)
         out_len = torch.zeros(nb, dtype=torch.int32, device=dev)
-        ci = torch.nonzero(~stored).flatten()
-        si = torch.nonzero(stored).flatten()
-        # stored blocks larger than their slot: the reference's RangeError (result.set)
-        over = size[si] > cap[si]
-        if si.numel():
-            status[si[over]] = -8
-        si = si[~over]
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(s):
-            e0.record(s)
-            if ci.numel():
-                c_in_off = pay_rel[ci].contiguous()
-                c_in_len = size[ci].to(torch.int32).contiguous()
-                c_out_off = slot_off[ci].contiguous()
-                c_cap = cap[ci].to(torch.int32).contiguous()
-                c_len = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
-                c_st = torch.zeros(ci.numel(), dtype=torch.int32, device=dev)
-                lz4mi.decompress_blocks_dev(rng.data_ptr(), c_in_off.data_ptr(), c_in_len.data_ptr(), out.data_ptr(),
-                                            c_out_off.data_ptr(), c_cap.data_ptr(), c_len.data_ptr(), c_st.data_ptr(),
-                                            ci.numel(), s.cuda_stream)
-            if si.numel():   # stored blocks: one launch (bufferDecompress.js:173-180), no per-block sync
-                s_in_off = pay_rel[si].contiguous()
-                s_len = size[si].to(torch.int32).contiguous()
-                s_out_off = slot_off[si].contiguous()
-                lz4mi.copy_stored_blocks_dev(rng.data_ptr(), rng.numel(), s_in_off.data_ptr(), s_len.data_ptr(),
-                                             s_out_off.data_ptr(), out.data_ptr(), out.numel(), si.numel(),
-                                             s.cuda_stream)
-            e1.record(s)
-            if ci.numel():
-                out_len[ci] = c_len
-                status[ci] = c_st
-            if si.numel():
-                out_len[si] = s_len
-        s.synchronize()
-        if ci.numel() or si.numel():
+        # every block in one launch: the size words go in as they are (LZ4MI_FRAME_WORDS), so a stored
+        # block (bit 31) is copied by its own wave beside the compressed ones (bufferDecompress.js:173-180;
+        # larger than its slot: the reference's RangeError, status -8)
+        if nb:
+            w32 = torch.where(word >= 2 ** 31, word - 2 ** 32, word).to(torch.int32).contiguous()
+            in_off = pay_rel.contiguous()
+            c_cap = cap.to(torch.int32).contiguous()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            s.wait_stream(torch.cuda.current_stream(dev))   # the tensors above were made on the current stream
+            with torch.cuda.stream(s):
+                e0.record(s)
+                lz4mi.decompress_blocks_dev(rng.data_ptr(), in_off.data_ptr(), w32.data_ptr(), out.data_ptr(),
+                                            slot_off.data_ptr(), c_cap.data_ptr(), out_len.data_ptr(),
+                                            status.data_ptr(), nb, s.cuda_stream, frame_words=True)
+                e1.record(s)
+            s.synchronize()
             self.last_kernel_s = e0.elapsed_time(e1) / 1e3
         if nb == 0:
             return torch.zeros(0, dtype=torch.uint8, device=dev), status

@@ -68,6 +68,10 @@ extern "C" {
 #define LZ4MI_XXH_LEN64 0x10u    /* streaming XXH32: keep the 64-bit total length (streams over 2 GiB);
                                     default: the reference class's `(totalLen + len) | 0` */
 #define LZ4MI_BLOCK_CHECKSUM 0x20u /* lz4mi_frame_pack: records carry XXH32 (spec) of their payload (FLG 0x10) */
+#define LZ4MI_FRAME_WORDS 0x40u  /* lz4mi_decompress_blocks (device pointers, not with LZ4MI_JS_COMPAT): in_len[b]
+                                    is the frame's raw size word; bit 31 set = a stored block, whose bytes are
+                                    copied in the same launch (bufferDecompress.js:173-180: LZ4MI_ERR_RANGE when
+                                    they exceed out_cap[b], the reference's result.set RangeError) */
 
 /* Largest block the kernels accept (the reference's largest block size is 4 MiB;
  * raw calls may pass more, up to 2^31-1 like the reference's `|0` arithmetic). */
@@ -259,17 +263,6 @@ int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_total, int64_
 int32_t lz4mi_frame_index(const uint8_t* frame, uint64_t len, uint64_t* pay_off, uint32_t* size_word,
                           uint32_t cap_blocks, int64_t* info, uint32_t flags, void* stream);
 
-/*
- * Stored (uncompressed) frame blocks into their output slots, one launch for all of them:
- * block b's n[b] bytes at frame + in_off[b] go to out + out_off[b] (clipped at the frame end
- * and at out_cap). Replaces the stored branch of the reference's frame loop
- * (src/buffer/bufferDecompress.js:173-180, result.set(input.subarray(...))); the caller
- * checks each block against its slot first (the reference's RangeError). Device pointers
- * only (LZ4MI_DEVICE_PTRS); asynchronous on `stream`.
- */
-int32_t lz4mi_copy_stored_blocks(const uint8_t* frame, uint64_t len, const uint64_t* in_off, const uint32_t* n,
-                                 const uint64_t* out_off, uint8_t* out, uint64_t out_cap, uint32_t nblocks,
-                                 uint32_t flags, void* stream);
 
 /*
  * Synthetic input generator (bench/test support, not a reference interface):

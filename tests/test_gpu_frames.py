@@ -103,8 +103,8 @@ def test_frame_checksum_waits_for_async_producer():
 def test_mostly_stored_frame_decodes_on_device():
     """a 16-block frame of 12 random (stored) + 4 tiles216 blocks — the
     GPU frame == the oracle's frame byte for byte, and the sharded device decode (stored blocks
-    copied by one lz4mi_copy_stored_blocks launch) returns the raw bytes; a stored block too
-    large for its slot reports the reference's RangeError."""
+    copied in the batch decode's own launch, LZ4MI_FRAME_WORDS) returns the raw bytes; a stored
+    block too large for its slot reports the reference's RangeError."""
     from lz4mi import frame as F
     n = 16
     kinds = ["random"] * 12 + ["tiles216"] * 4
@@ -131,6 +131,16 @@ def test_mostly_stored_frame_decodes_on_device():
     last = n - 1
     want = -8 if int(word[last]) & 0x80000000 else 0
     assert int(st[last]) in (want, -1) and all(int(x) == 0 for x in st[:last].tolist())
+
+
+def test_frame_words_flag_contract():
+    """LZ4MI_FRAME_WORDS needs device pointers and the batch kernel (not LZ4MI_JS_COMPAT)."""
+    L = lz4mi.lib()
+    z = torch.zeros(64, dtype=torch.int64, device="cuda")
+    p = z.data_ptr()
+    fl = lz4mi.DEVICE_PTRS | lz4mi.FRAME_WORDS
+    assert L.lz4mi_decompress_blocks(p, p, p, p, p, p, None, 0, p, p, 1, fl | lz4mi.JS_COMPAT, None) == lz4mi.ERR_ARG
+    assert L.lz4mi_decompress_blocks(p, p, p, p, p, p, None, 0, p, p, 0, fl, None) == lz4mi.OK
 
 
 def test_decoder_workspace_aliasing():
