@@ -69,44 +69,15 @@ __device__ __forceinline__ uint32_t src_byte(const CompJob& j, int64_t p) {
     return (p >= 0 && (uint64_t)p < j.src_total) ? (uint32_t)j.src[p] : 0u;
 }
 
-#ifndef LZ4MI_EMIT_LANES
-#define LZ4MI_EMIT_LANES 1   // a batch's sequences written by their own lanes (4 byte stores); 0: one lane per output byte
-#endif
-#ifndef LZ4MI_SHFL_READLANE
-#define LZ4MI_SHFL_READLANE 0   // 1: the two per-batch lane gathers as v_readlane (measured slower: SGPR spills)
-#endif
-
-// Lanes 8g .. 8g+7 get v of lane g (g < 8): eight v_readlane, no LDS permute round trip.
-__device__ __forceinline__ int32_t group_val(int32_t v, int g) {
-#if LZ4MI_SHFL_READLANE
-    int32_t r = -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int32_t x = (int32_t)__builtin_amdgcn_readlane((uint32_t)v, k);
-        r = g == k ? x : r;
-    }
-    return r;
-#else
-    return __shfl(v, g, kWave);
-#endif
-}
+// Lanes 8g .. 8g+7 get v of lane g (g < 8): one LDS permute (eight v_readlane instead were slower:
+// SGPR spills, round 4).
+__device__ __forceinline__ int32_t group_val(int32_t v, int g) { return __shfl(v, g, kWave); }
 
 // Lane l gets v of lane 8 (l & 7) + f, f = the first set bit of byte (l & 7) of mm (0 when
-// the byte is 0; `ft` is that lane's own f): per group one scalar bit search + v_readlane.
+// the byte is 0; `ft` is that lane's own f): one LDS permute.
 __device__ __forceinline__ uint32_t first_val(uint32_t v, uint64_t mm, int lane, int ft) {
-#if LZ4MI_SHFL_READLANE
-    (void)ft;
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t gk = (uint32_t)(mm >> (8 * k)) & 0xFFu;
-        const uint32_t x = __builtin_amdgcn_readlane(v, 8 * k + (gk ? __builtin_ctz(gk) : 0));
-        r = (lane & 7) == k ? x : r;
-    }
-    return r;
-#else
+    (void)mm;
     return __shfl(v, 8 * (lane & 7) + ft, kWave);
-#endif
 }
 
 // Value of v in lane l, l uniform (a ballot's ctz, a lane count): v_readlane
@@ -432,7 +403,6 @@ __device__ __forceinline__ void ring_seqs(SH& F, FastOut& o, int lane, int npend
     const bool mine = lane < npend;
     const int32_t lit = lane == 0 ? lit0 : 0;
     ring_reserve(F, o, lane, total);
-#if LZ4MI_EMIT_LANES
     // each sequence's own lane writes its token, offset and length byte; lanes 1 .. lit0 the
     // literal bytes of sequence 0 (which starts the batch)
     const uint32_t base = (uint32_t)o.op, msk = (uint32_t)RING_MASK(F);
@@ -444,31 +414,6 @@ __device__ __forceinline__ void ring_seqs(SH& F, FastOut& o, int lane, int npend
         if (mcode >= 15) F.ring[(b + 2u) & msk] = (uint8_t)(mcode - 15);
     }
     if (lane >= 1 && lane <= lit0) F.ring[(base + (uint32_t)lane) & msk] = (uint8_t)litv;
-#else
-    // output lane t finds its sequence among the <= 8 starts and writes byte t
-    const uint32_t tok = ((uint32_t)lit << 4) | (mcode >= 15 ? 15u : (uint32_t)mcode);
-    int32_t r = lane, cl = 0;
-    uint32_t ct = 0, co = 0, cm = 0;
-    for (int k = 0; k < npend; ++k) {
-        const int32_t sk = (int32_t)lane_val(start, k);
-        if (lane >= sk) {
-            r = lane - sk;
-            cl = k == 0 ? lit0 : 0;
-            ct = lane_val(tok, k);
-            co = lane_val(off, k);
-            cm = (uint32_t)lane_val(mcode, k);
-        }
-    }
-    if (lane < total) {
-        uint32_t v;
-        if (r == 0) v = ct;
-        else if (r <= cl) v = litv;
-        else if (r == cl + 1) v = co & 255;
-        else if (r == cl + 2) v = (co >> 8) & 255;
-        else v = cm - 15;
-        F.ring[(o.op + lane) & RING_MASK(F)] = (uint8_t)v;
-    }
-#endif
     o.op += total;
 }
 
@@ -537,30 +482,14 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
 #ifndef LZ4MI_DUPSLOT
 #define LZ4MI_DUPSLOT 1   // hit batches test for repeated hashes with an LDS slot before the DPP checks (A/B switch)
 #endif
-#ifndef LZ4MI_OFF32
-#define LZ4MI_OFF32 0   // 1: batch encoder loads as 32-bit offsets from the block base (measured slower: 77.9 vs 74.9 ms)
-#endif
-// The batch encoder's loads (blocks < 2^31 bytes, lim = the block's length): 32-bit bounds
-// tests and a 32-bit unsigned offset from the block's (scalar) base, so the load takes the
-// scalar-base form instead of a 64-bit per-lane address. Zero outside [0, lim).
+// The batch encoder's loads (zero outside the block). 32-bit offsets from the block's scalar
+// base instead were slower (77.9 vs 74.9 ms, round 4).
 __device__ __forceinline__ uint4 ld16o(const CompJob& j, uint32_t lim, int32_t p) {
-#if LZ4MI_OFF32
-    if ((uint32_t)p < lim && lim - (uint32_t)p >= 16u) {
-        uint4 v;
-        __builtin_memcpy(&v, j.src + (uint32_t)p, 16);
-        return v;
-    }
-#endif
+    (void)lim;
     return ld16(j, p);
 }
 __device__ __forceinline__ uint32_t ld_u32o(const CompJob& j, uint32_t lim, int32_t p) {
-#if LZ4MI_OFF32
-    if ((uint32_t)p < lim && lim - (uint32_t)p >= 4u) {
-        uint32_t v;
-        __builtin_memcpy(&v, j.src + (uint32_t)p, 4);
-        return v;
-    }
-#endif
+    (void)lim;
     return ld_u32(j, p);
 }
 
