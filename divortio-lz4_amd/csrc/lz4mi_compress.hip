@@ -222,8 +222,8 @@ __device__ __forceinline__ void settle32(uint32_t& v) { asm volatile("" : "+v"(v
 // earlier lane's (found by writing lane ids into the table and reading them
 // back), so the batch's inserts never interact and the result is the serial one.
 //
-// Output goes to a 4 KiB LDS ring flushed in 16-byte units; long literal runs
-// are copied global -> global directly. No vector-memory store precedes the
+// Output goes to an LDS ring (4 KiB; 2 KiB in the batch encoder) flushed in 16-byte
+// units; literal runs longer than the ring takes are copied global -> global directly. No vector-memory store precedes the
 // next probe's loads except at ring flushes.
 constexpr int kCodeWords = 16384 / 16;
 #define RING_SZ(F) ((int64_t)sizeof((F).ring))   // the output ring's size in the caller's shared struct
@@ -285,7 +285,10 @@ __device__ __forceinline__ void ring_len_ext(SH& F, FastOut& o, int lane, int64_
 template <class SH, class SRC = SrcG>
 __device__ void ring_copy(SH& F, FastOut& o, const CompJob& j, int lane, int64_t pos, int64_t n,
                           const Ring* rg = nullptr) {
-    if (n > kDirectLit) {
+    // a run through the ring must fit beside the <= 15 bytes a flush leaves pending: the
+    // batch encoder's 2 KiB ring takes at most 2032 (2034..2048 wrapped onto those bytes)
+    constexpr int64_t kViaRing = RING_SZ(F) - 16 < kDirectLit ? RING_SZ(F) - 16 : kDirectLit;
+    if (n > kViaRing) {
         // head into the ring up to a 16-byte boundary, flush, bulk direct, tail into the ring
         const int64_t h = (16 - (o.op & 15)) & 15;
         ring_reserve(F, o, lane, 16);

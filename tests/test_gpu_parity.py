@@ -370,3 +370,43 @@ def test_compress_chain_dependent_blocks_match_oracle(bs):
             b += 1
         assert b == len(got)
         assert np.array_equal(t_gpu, t_ref), (bs, start)
+
+
+def _lit_run_blocks():
+    """Blocks whose literal runs sweep the batch encoder's 2 KiB output ring: random runs of
+    2000..2100 bytes between zero runs (every count of bytes a ring flush leaves pending),
+    final runs of 2016..2064 bytes, and the `far` data (8-48 KiB copies from the previous
+    64 KiB, tools/microbench.py) that showed a 2034..2048-byte run wrapping the ring."""
+    rng = np.random.default_rng(77)
+    parts = [rng.integers(0, 256, 4096, dtype=np.uint8)]
+    for L in range(2000, 2101):
+        parts.append(rng.integers(1, 256, L, dtype=np.uint8))
+        parts.append(np.zeros(40 + L % 23, dtype=np.uint8))
+    blocks = [np.concatenate(parts)]
+    for L in range(2016, 2065, 3):
+        head = np.concatenate([rng.integers(0, 256, 3000, dtype=np.uint8), np.zeros(L % 37 + 20, dtype=np.uint8)])
+        blocks.append(np.concatenate([head, rng.integers(0, 256, L, dtype=np.uint8)]))
+    for _ in range(2):
+        b = np.empty(1 << 20, dtype=np.uint8)
+        b[:65536] = rng.integers(0, 256, 65536, dtype=np.uint8)
+        pos = 65536
+        while pos < b.size:
+            ln = min(int(rng.integers(8192, 49152)), b.size - pos)
+            src = pos - int(rng.integers(ln, 65536))
+            b[pos:pos + ln] = b[src:src + ln]
+            pos += ln
+        blocks.append(b)
+    return blocks
+
+
+def test_compress_literal_runs_around_ring_size():
+    """Batch encoder vs the oracle, byte-exact, on literal runs about the output ring's size
+    (lz4mi_compress.hip ring_copy), and the GPU decode of its output round-trips."""
+    blocks = _lit_run_blocks()
+    comps = lz4mi.compress_blocks(blocks)
+    for k, (b, c) in enumerate(zip(blocks, comps)):
+        ref = O.compress_block_bytes(b)
+        assert c.size == ref.size and np.array_equal(c, ref), k
+    st, outs, lens = lz4mi.decompress_blocks(comps, [b.size for b in blocks])
+    for k, (b, o) in enumerate(zip(blocks, outs)):
+        assert st[k] == 0 and np.array_equal(o, b), k
