@@ -25,6 +25,10 @@
 extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                               const uint64_t*, const uint32_t*, const uint8_t*, uint32_t, uint32_t*,
                                               int32_t*, uint32_t, int, uint32_t*, hipStream_t);
+extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
+                                                    const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
+                                                    uint32_t*, int32_t*, uint32_t, uint32_t, uint32_t, void*, hipStream_t);
+extern "C" size_t lz4mi_small_scratch_bytes(uint32_t, uint32_t, uint32_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
 extern "C" hipError_t lz4mi_launch_frame_pack(const uint8_t*, const uint64_t*, const uint32_t*, const uint8_t*,
@@ -81,18 +85,20 @@ struct StreamCtx {
     Scratch frame_meta;   // block-checksum payload offsets / lengths of frame_pack
     Scratch scan;         // frame_decompress: block lists of the device frame walk
     Scratch order;        // batch decode: the blocks' dispatch order (lz4mi_block_order_kernel)
+    Scratch small;        // small-batch decode: exported sequences and output pointers (lz4mi_expand.hip)
     void release() {
         tables.release();
         frame_meta.release();
         scan.release();
         order.release();
+        small.release();
     }
 };
 
 struct Ctx {
     std::atomic<int> device{-1};   // set once by init_locked, never changed after
     hipStream_t stream = nullptr;
-    Scratch in, out, meta, aux, order;   // staging of the synchronous host-pointer entry points
+    Scratch in, out, meta, aux, order, small;   // staging of the synchronous host-pointer entry points
     std::mutex mu;                // serialises the host-pointer entry points (their staging is shared)
     std::mutex streams_mu;
     std::vector<std::unique_ptr<StreamCtx>> streams;
@@ -144,12 +150,30 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
+// Small batches (at most this many blocks, LZ4 spec mode) decode by pointer jumping over the
+// whole GPU (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB block's latency
+// is then its parse, not its chain of copies. LZ4MI_SMALL_BLOCKS=0 turns it off.
+constexpr uint32_t kSmallInMax = (4u << 20) + (4u << 20) / 255 + 16;   // a 4 MiB block's compress bound
+constexpr uint32_t kSmallOutMax = 4u << 20;
+uint32_t small_blocks() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("LZ4MI_SMALL_BLOCKS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16u;
+    }();
+    return n;
+}
+
 // `order`: scratch of nblocks words for the dispatch order, owned by the caller's lock
-// (nullptr: the blocks go in index order)
+// (nullptr: the blocks go in index order); `small`: the small-batch path's scratch (nullptr:
+// never taken)
 hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
-                         Scratch* order) {
+                         Scratch* order, Scratch* small = nullptr) {
+    if (small && mode == 0 && nblocks <= small_blocks() &&
+        small->ensure(lz4mi_small_scratch_bytes(nblocks, kSmallInMax, kSmallOutMax), s) == hipSuccess)
+        return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
+                                             status, nblocks, kSmallInMax, kSmallOutMax, small->p, s);
     uint32_t* ord = nullptr;
     if (order && nblocks > 1 && order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
@@ -348,7 +372,7 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
         StreamCtx* c = stream_ctx(s);
         std::lock_guard<std::mutex> sl(c->mu);
         LZ4MI_TRY(decode_launch(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
-                                mode, s, &c->order));
+                                mode, s, &c->order, &c->small));
         return LZ4MI_OK;
     }
     if (!in || !out || !in_off || !in_len || !out_off || !out_cap || !out_len || !status) return LZ4MI_ERR_ARG;
@@ -402,7 +426,7 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off, m_out_cap,
                             dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks, mode, s,
-                            &g_ctx.order));
+                            &g_ctx.order, &g_ctx.small));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));

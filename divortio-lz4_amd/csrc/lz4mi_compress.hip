@@ -482,6 +482,15 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
     return make_uint4(ld_u32(j, p), ld_u32(j, p + 4), ld_u32(j, p + 8), ld_u32(j, p + 12));
 }
 
+#ifndef LZ4MI_LDS_TABLE
+#define LZ4MI_LDS_TABLE 0 // 1: the batch encoder's position table in LDS instead of global (A/B switch)
+#endif
+#ifndef LZ4MI_KMAX
+#define LZ4MI_KMAX 8      // probes per hit batch (<= kSpecK) (A/B switch)
+#endif
+#ifndef LZ4MI_KADAPT
+#define LZ4MI_KADAPT 0    // 1: next hit batch K = J + 2 after a batch ended at probe J < K - 1; 2: 2 (J + 1) (A/B switch)
+#endif
 #ifndef LZ4MI_DUPSLOT
 #define LZ4MI_DUPSLOT 1   // hit batches test for repeated hashes with an LDS slot before the DPP checks (A/B switch)
 #endif
@@ -510,6 +519,9 @@ struct GtsShared {
     uint8_t slot[1024];                  // miss batches: lane ids keyed by hash & 1023
     uint32_t code[kCodeWords];           // 2-bit epoch code per table entry
     uint32_t win[kWinBytes / 4 + 4];     // source bytes [wb, wb + kWinBytes)
+#if LZ4MI_LDS_TABLE
+    uint16_t tab[16384];                 // the 15-bit table in LDS (41 KB per block: 3 blocks per CU)
+#endif
 };
 
 __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T, int lane) {
@@ -520,13 +532,22 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     int32_t i = 0, anchor = 0;
     uint32_t c = 67;
     int32_t S = 0;                       // step of the last hit (0: in a miss chain): the speculated probe distance
-    const int kmax = kSpecK;
+#if LZ4MI_KADAPT
+    int kmax = LZ4MI_KMAX;               // probes of the next hit batch, sized from how far the last one got
+#else
+    const int kmax = LZ4MI_KMAX;
+#endif
     // accepted sequences not emitted yet (lanes 0 .. npend-1: probe, candidate, match end),
     // emitted while the next batch's table reads are in flight
     int npend = 0;
     int32_t pd_p = 0, pd_c = 0, pd_e = 0;
     int32_t wb = -(1 << 30);             // F.win holds source [wb, wb + kWinBytes)
+#if LZ4MI_LDS_TABLE
+    uint16_t* T16 = F.tab;
+    (void)T;
+#else
     uint16_t* T16 = (uint16_t*)T;
+#endif
     int32_t g = 0;
     for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
     for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
@@ -726,6 +747,11 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             insert(lane <= J && !later, h, p);
             const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
             const bool hitJ = (__ballot(hit) >> J) & 1ull;
+#if LZ4MI_KADAPT == 1
+            kmax = J + 1 >= K ? LZ4MI_KMAX : min(LZ4MI_KMAX, J + 2);
+#elif LZ4MI_KADAPT == 2
+            kmax = J + 1 >= K ? LZ4MI_KMAX : min(LZ4MI_KMAX, 2 * (J + 1));
+#endif
             pd_p = p;
             pd_c = cand;
             pd_e = e;
@@ -803,6 +829,9 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         const int mi = nprobe - 1;
         const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
         c = 67;
+#if LZ4MI_KADAPT
+        kmax = LZ4MI_KMAX;
+#endif
         const int32_t e1 = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
         pd_p = pm;
         pd_c = cm;

@@ -1196,6 +1196,10 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         }
         return;
     }
+    // small-batch export (lz4mi_expand.hip): the parse only, the sequences to xseq
+    const bool xp = a.xseq && !a.f1check && !a.frame_words && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max;
+    uint4* const xs = xp ? a.xseq + (size_t)b * a.xseq_stride : nullptr;
+    uint32_t nx = 0;
 #if LZ4MI_LL_ADAPT
     const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
     unsigned int* lat = &g_lat_active[32 * xcc_id()];
@@ -1488,6 +1492,27 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             cq = q;
         }
         const int64_t tab_hi = c.O + total;
+        if (xp) {   // export: the table's sequences (output start, literal source, lengths, offset)
+            for (uint32_t k = lane; k < nseq; k += kWave) {
+                const SeqInfo q = seq_info(S, k);
+                xs[nx + k] = make_uint4((uint32_t)q.out, (uint32_t)(c.ip + q.lit), (uint32_t)q.ll,
+                                        q.ml ? (uint32_t)q.off : 0u);
+            }
+            nx += nseq;
+            if (cut) {
+                const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
+                if (e) { status = err_status(e); break; }
+                if (lane == 0) xs[nx] = make_uint4((uint32_t)tab_hi, (uint32_t)clit, (uint32_t)cll, cml ? coff : 0u);
+                ++nx;
+                c.O = tab_hi + cll + cml;
+                c.ip = (int32_t)(cq < c.in_len ? cq : c.in_len);
+            } else {
+                c.O = tab_hi;
+                c.ip = tail >= kEnd ? c.in_len : c.ip + (int32_t)tail;
+            }
+            __syncthreads();
+            continue;
+        }
         if (cut) {   // the next chunk's bytes: their loads go out before this chunk's stores
             int64_t nip = cq < c.in_len ? cq : c.in_len;
             if (nip < c.in_len) {
@@ -1692,6 +1717,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     if (lane == 0) {
         a.status[b] = status;
         a.out_len[b] = status ? 0u : (uint32_t)c.O;
+        if (a.xcnt) a.xcnt[b] = xp ? nx : kNotExported;
     }
 #if LZ4MI_LL_ADAPT
     if (lat_bound && lane == 0) atomicSub(lat, 1u);
@@ -1804,4 +1830,49 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
     }
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     return hipGetLastError();
+}
+
+extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, uint8_t*, const uint64_t*, const uint32_t*,
+                                          const uint8_t*, uint32_t, const uint32_t*, const int32_t*, const uint4*,
+                                          const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*, uint32_t,
+                                          hipStream_t);
+
+// A small batch in LZ4 spec mode (lz4mi_expand.hip): each block within the export limits
+// (x_in_max compressed, x_out_max output bytes) is parsed by the batch kernel, which exports
+// its sequences instead of writing them; the whole GPU then computes the output by pointer
+// jumping. Other blocks are decoded by the same launch as usual. `xs` scratch:
+// nblocks * xseq_stride sequence entries, nblocks counts, nblocks * x_out_max pointers and
+// the jump rounds' flags (lz4mi_small_scratch_bytes).
+extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
+    const size_t stride = x_in_max / 3 + 8;
+    return ((size_t)nblocks * stride * 16 + 255) / 256 * 256 + ((size_t)nblocks * 4 + 255) / 256 * 256 +
+           (size_t)nblocks * x_out_max * 4 + 256;
+}
+extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                                    uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                                    const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
+                                                    int32_t* status, uint32_t nblocks, uint32_t x_in_max,
+                                                    uint32_t x_out_max, void* xs, hipStream_t stream) {
+    if (nblocks == 0) return hipSuccess;
+    const uint32_t stride = x_in_max / 3 + 8;
+    uint8_t* p = (uint8_t*)xs;
+    uint4* xseq = (uint4*)p;
+    p += ((size_t)nblocks * stride * 16 + 255) / 256 * 256;
+    uint32_t* xcnt = (uint32_t*)p;
+    p += ((size_t)nblocks * 4 + 255) / 256 * 256;
+    uint32_t* ptr = (uint32_t*)p;
+    p += (size_t)nblocks * x_out_max * 4;
+    uint32_t* flags = (uint32_t*)p;
+    lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
+                     nblocks > 1 ? 1 : 0, 0};
+    a.xseq = xseq;
+    a.xcnt = xcnt;
+    a.xseq_stride = stride;
+    a.x_in_max = x_in_max;
+    a.x_out_max = x_out_max;
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, stride,
+                               ptr, x_out_max, flags, nblocks, stream);
 }

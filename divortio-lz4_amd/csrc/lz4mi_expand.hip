@@ -1,0 +1,193 @@
+// lz4mi_expand.hip — the output of a small batch (few blocks) by pointer jumping.
+//
+// The batch decoder (lz4mi_decompress.hip) writes a block with one wave: a 4 MiB tiles216
+// block alone takes ~8 ms, the latency of that wave's chain, however idle the rest of the
+// GPU is. Here a block's output is computed by the whole GPU instead, once its sequence
+// table is known (the decoder's parse, run in export mode: DecArgs::xseq):
+//
+//   expand: every output byte x gets a source pointer: a literal byte -> its position in the
+//           compressed block (resolved), a match byte -> x - offset, an earlier output byte
+//           (unresolved) or a byte before the block (caller's history / dictionary: resolved);
+//   jump:   ptr[x] = ptr[ptr[x]] for every unresolved x, in place, round after round; each
+//           round at least doubles the hops a pointer has taken, so a chain of D matches is
+//           resolved in ceil(log2 D) + 1 rounds (tiles216: D <= 332, 10 rounds; text: 21 489, 16;
+//           a byte of an overlapping match points into the period before the match, so every
+//           hop lands in an earlier sequence: D < 2^20 sequences of a <= 4 MiB block, 21
+//           rounds). Pointers only point
+//           backwards and every value on a chain resolves to the same byte, so reading a
+//           pointer another thread has just replaced (or not yet) is correct either way;
+//   gather: out[x] = the byte the resolved pointer names.
+//
+// The reference decoder (blockDecompress.js:55-272) copies the same bytes in sequence
+// order; the result is identical because every output byte is a copy of exactly one
+// literal (or history/dictionary) byte, found by following the matches backwards.
+// Memory per block: 4 bytes per output byte (pointers) + 16 bytes per sequence.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz4mi_decompress.h"
+
+namespace lz4mi {
+
+constexpr uint32_t kUnres = 0x80000000u;   // ptr < kUnres: an output position still to follow
+constexpr uint32_t kLit = 0x80000000u;     // kLit | p: byte p of the compressed block
+constexpr uint32_t kHist = 0xC0000000u;    // kHist | (y + 65536): byte y < 0 before the block
+constexpr int kXThreads = 256;
+constexpr int kXBytes = 16;                // output bytes per thread
+constexpr int kJumpRounds = 21;
+
+struct ExpArgs {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint32_t* out_cap;
+    const uint8_t* dict;
+    uint32_t dict_len;
+    const uint32_t* out_len;
+    const int32_t* status;
+    const uint4* xseq;
+    const uint32_t* xcnt;
+    uint32_t xseq_stride;
+    uint32_t* ptr;            // x_out_max pointers per block
+    uint32_t x_out_max;
+    uint32_t* flags;          // flags[r]: round r has unresolved pointers to follow
+};
+
+// This thread's 16 output bytes [x0, x0 + 16) of block blockIdx.y, and n = the block's
+// output length (0: nothing to do here)
+__device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t& x0) {
+    const uint32_t b = blockIdx.y;
+    if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return 0;
+    const uint32_t n = min(a.out_len[b], a.out_cap[b]);
+    x0 = (blockIdx.x * kXThreads + threadIdx.x) * kXBytes;
+    return x0 < n ? n : 0u;
+}
+
+__global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
+    uint32_t x0;
+    const uint32_t n = x_span(a, x0);
+    if (!n) return;
+    const uint32_t b = blockIdx.y;
+    const uint4* S = a.xseq + (size_t)b * a.xseq_stride;
+    const uint32_t cnt = a.xcnt[b];
+    // the last sequence starting at or before x0
+    uint32_t lo = 0, hi = cnt;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (S[mid].x <= x0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t k = lo;
+    uint4 e = S[k];
+    uint32_t nxt = k + 1 < cnt ? S[k + 1].x : 0xFFFFFFFFu;
+    uint32_t v[kXBytes];
+    bool unres = false;
+#pragma unroll
+    for (int t = 0; t < kXBytes; ++t) {
+        const uint32_t x = x0 + t;
+        while (x >= nxt) {
+            ++k;
+            e = S[k];
+            nxt = k + 1 < cnt ? S[k + 1].x : 0xFFFFFFFFu;
+        }
+        if (x - e.x < e.z) {
+            v[t] = kLit | (e.y + (x - e.x));
+        } else {
+            // an overlapping match repeats its first `offset` bytes: point into the period
+            // before the match start, so every pointer lands in an earlier sequence (a chain
+            // hops at most once per sequence, not once per period)
+            const uint32_t ms = e.x + e.z, d = x - ms;
+            const int32_t y = (int32_t)(d < e.w ? x : ms + d % e.w) - (int32_t)e.w;
+            v[t] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
+            unres |= y >= 0 && x < n;
+        }
+    }
+    uint4* P = (uint4*)(a.ptr + (size_t)b * a.x_out_max + x0);
+#pragma unroll
+    for (int q = 0; q < kXBytes / 4; ++q) P[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    if (unres) a.flags[0] = 1u;
+}
+
+__global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r) {
+    if (a.flags[r] == 0) return;
+    uint32_t x0;
+    const uint32_t n = x_span(a, x0);
+    if (!n) return;
+    uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
+    uint4 w[kXBytes / 4];
+#pragma unroll
+    for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
+    uint32_t* v = (uint32_t*)w;
+    uint32_t u[kXBytes];
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
+#pragma unroll
+    for (int t = 0; t < kXBytes; ++t) {
+        any |= u[t] != v[t];
+        v[t] = u[t];
+    }
+    if (!any) return;
+#pragma unroll
+    for (int q = 0; q < kXBytes / 4; ++q) ((uint4*)(P + x0))[q] = w[q];
+    bool still = false;
+#pragma unroll
+    for (int t = 0; t < kXBytes; ++t) still |= v[t] < kUnres && x0 + t < n;
+    if (still) a.flags[r + 1] = 1u;
+}
+
+__global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
+    uint32_t x0;
+    const uint32_t n = x_span(a, x0);
+    if (!n) return;
+    const uint32_t b = blockIdx.y;
+    const uint32_t* P = a.ptr + (size_t)b * a.x_out_max + x0;
+    const uint8_t* src = a.in + a.in_off[b];
+    uint8_t* dst = a.out + a.out_off[b];
+    const int64_t out_off = (int64_t)a.out_off[b];
+    uint4 w[kXBytes / 4];
+#pragma unroll
+    for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)P)[q];
+    const uint32_t* v = (const uint32_t*)w;
+    uint32_t o[kXBytes / 4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < kXBytes; ++t) {
+        uint32_t c = 0;
+        if ((v[t] & kHist) == kHist) {            // before the block: the caller's bytes or the dictionary
+            const int64_t y = (int64_t)(v[t] & 0x3FFFFFFFu) - 65536;
+            c = out_off + y >= 0 ? dst[y] : (a.dict ? a.dict[(int64_t)a.dict_len + out_off + y] : 0u);
+        } else if (v[t] & kLit) {
+            c = src[v[t] & 0x3FFFFFFFu];
+        }
+        o[t >> 2] |= c << (8 * (t & 3));
+    }
+    if (x0 + kXBytes <= n) {
+        *(uint4*)(dst + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+        for (uint32_t t = 0; x0 + t < n; ++t) dst[x0 + t] = (uint8_t)(o[t >> 2] >> (8 * (t & 3)));
+    }
+}
+
+}  // namespace lz4mi
+
+// The output phase of an exported small batch: expand, up to kJumpRounds jump rounds (each
+// returns at once when the previous one left nothing to follow), gather. `flags`: scratch of
+// kJumpRounds + 1 words.
+extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, uint8_t* out,
+                                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
+                                          uint32_t dict_len, const uint32_t* out_len, const int32_t* status,
+                                          const uint4* xseq, const uint32_t* xcnt, uint32_t xseq_stride, uint32_t* ptr,
+                                          uint32_t x_out_max, uint32_t* flags, uint32_t nblocks, hipStream_t stream) {
+    using namespace lz4mi;
+    if (nblocks == 0) return hipSuccess;
+    ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xseq_stride, ptr,
+              x_out_max, flags};
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * (kJumpRounds + 1), stream);
+    if (e != hipSuccess) return e;
+    const dim3 grid((x_out_max + kXThreads * kXBytes - 1) / (kXThreads * kXBytes), nblocks);
+    hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
+    for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
+    hipLaunchKernelGGL(lz4mi_gather_kernel, grid, dim3(kXThreads), 0, stream, a);
+    return hipGetLastError();
+}

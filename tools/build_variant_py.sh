@@ -13,7 +13,7 @@ python3 "$py" $T/$F0
 mkdir -p $R/tools/variants
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include $*"
 objs=""
-for f in lz4mi_decompress.hip lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_frame.hip lz4mi_capi.cpp; do
+for f in lz4mi_decompress.hip lz4mi_expand.hip lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_frame.hip lz4mi_capi.cpp; do
   if [ "$f" = "$F0" ]; then srcf=$T/$f; else srcf=$C/$f; fi
   /opt/rocm/bin/hipcc $F -c -o $T/$f.o $srcf & objs="$objs $T/$f.o"
 done
