@@ -21,14 +21,32 @@ struct DecArgs {
     int f1check;   // reference-exact (LZ4MI_JS_EXACT): fix up every chunk the reference's F1 rewrite changes
     const uint32_t* order = nullptr;   // workgroup w decodes block order[w] (nullptr: block w)
     int frame_words = 0;               // in_len[b] is a frame size word: bit 31 = stored block (copied)
-    // small batches (lz4mi_expand.hip): a block within the export limits is parsed only and its
-    // sequences exported as {output start, literal source, literal length, offset} to
-    // xseq + b * xseq_stride, their count to xcnt[b] (kNotExported: decoded here as usual)
+    // small batches (lz4mi_expand.hip, lz4mi_decompress_x_kernel): a block within the export
+    // limits is parsed by xsegs waves, one per segment of its compressed bytes, which export
+    // their sequences as {output start in the segment, literal source, literal length, offset}
+    // to xseq + (b * xsegs + s) * xseq_stride and their summary to xrec[b * xsegs + s]; a block
+    // past the limits is decoded by its segment-0 wave as usual (xcnt[b] = kNotExported)
     uint4* xseq = nullptr;
     uint32_t* xcnt = nullptr;
-    uint32_t xseq_stride = 0;          // entries per block (>= in_len / 3 + 2 for an exported block)
+    struct SegRec* xrec = nullptr;
+    uint32_t xseq_stride = 0;          // entries per segment
+    uint32_t xsegs = 0;
     uint32_t x_in_max = 0, x_out_max = 0;
 };
+// One segment of an exported block. Its wave parses from a guessed entry (the first token at or
+// past the segment start, found by a warm-up parse 4 KiB before it), then checks the guess
+// against the previous segment's final exit and re-parses from that exit when they differ.
+struct SegRec {
+    uint32_t entry;   // first token at or past the segment start (the chain's end: in_len)
+    uint32_t exit;    // first token at or past the segment end
+    uint32_t cnt;     // sequences exported (incl. a failing one)
+    uint32_t olen;    // their output bytes
+    uint32_t err;     // (index in the segment << 3) | check of its first parse error; 0xFFFFFFFF: none
+    uint32_t fin;     // final exit + 1 once checked against the previous segment (0: not yet)
+    uint32_t base;    // output start of the segment (lz4mi_xcheck_kernel)
+    uint32_t pad;
+};
+constexpr uint32_t kFinErr = 0xFFFFFFFEu;   // fin - 1 of a segment at or after the block's first error
 constexpr uint32_t kNotExported = 0xFFFFFFFFu;
 
 }  // namespace lz4mi

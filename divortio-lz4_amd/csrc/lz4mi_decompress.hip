@@ -1081,6 +1081,18 @@ __device__ __forceinline__ uint32_t seq_error(const Ctx& c, int64_t out_start, i
 }
 
 __device__ __forceinline__ int32_t err_status(uint32_t e) { return e == 5 ? -9 : -(int32_t)e; }
+// An exported segment (XP, rel) knows only its relative output positions: checks 2 and 3 here,
+// 1, 4 and 5 after the parse (lz4mi_xcheck_kernel), in the same order per sequence.
+template <bool XP>
+__device__ __forceinline__ uint32_t seq_err(const Ctx& c, bool rel, int64_t out_start, int64_t lit, int64_t ll,
+                                            uint32_t off, int64_t ml) {
+    if (XP && rel) {
+        if (lit + ll > c.in_len) return 2;
+        if (ml == 0) return 0;
+        return off == 0 ? 3u : 0u;
+    }
+    return seq_error(c, out_start, lit, ll, off, ml);
+}
 
 // Would the reference's double-copy-tail rewrite (src/block/blockDecompress.js:219-250,
 // offset >= 8, length < 8, source in the output) change a byte of
@@ -1153,11 +1165,15 @@ __device__ void f1_fixup(const Ctx c, const DecShared& S, int lane, uint32_t nse
     }
 }
 
+template <bool XP>
 __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     __shared__ DecShared S;
     const int lane = threadIdx.x;
-    if (blockIdx.x >= a.nblocks) return;
-    const uint32_t b = a.order ? uniform(a.order[blockIdx.x]) : blockIdx.x;
+    const uint32_t nseg = XP ? a.xsegs : 1u;   // XP: waves per block (one per segment)
+    if (blockIdx.x >= a.nblocks * nseg) return;
+    const uint32_t wblk = XP ? blockIdx.x / nseg : blockIdx.x;
+    const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;
+    const uint32_t b = a.order ? uniform(a.order[wblk]) : wblk;
 #if LZ4MI_TIMELINE
     const uint64_t tl_t0 = wall_clock64();
 #endif
@@ -1196,10 +1212,26 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         }
         return;
     }
-    // small-batch export (lz4mi_expand.hip): the parse only, the sequences to xseq
-    const bool xp = a.xseq && !a.f1check && !a.frame_words && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max;
-    uint4* const xs = xp ? a.xseq + (size_t)b * a.xseq_stride : nullptr;
-    uint32_t nx = 0;
+    // small-batch export (XP, lz4mi_expand.hip): segment sg of the block, parsed only
+    const bool xp = XP && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max;
+    if (XP && !xp && sg != 0) return;   // past the export limits: its segment-0 wave decodes it as usual
+    uint4* xs = nullptr;
+    SegRec* xr = nullptr;
+    uint32_t seg_lo = 0, seg_hi = 0;    // the segment: tokens in [seg_lo, seg_hi)
+    if (XP && xp) {
+        const uint32_t L = max(4096u, (((uint32_t)c.in_len + nseg - 1) / nseg + 1023u) & ~1023u);
+        seg_lo = sg * L;
+        seg_hi = sg + 1 == nseg ? (uint32_t)c.in_len : min((uint32_t)c.in_len, seg_lo + L);
+        xs = a.xseq + ((size_t)wblk * nseg + sg) * a.xseq_stride;
+        xr = a.xrec + (size_t)wblk * nseg + sg;
+    }
+    // export state (uniform): the entry found, done, the speculation failed, entry / exit tokens,
+    // sequences exported, their output bytes, the first parse error; x_OG: output position of
+    // the entry in this wave's running count; pass 1: the exact re-parse from x_entry
+    bool x_started = false, x_done = false, x_fail = false;
+    uint32_t x_G = 0, x_X = 0, nx = 0, x_olen = 0, x_err = 0xFFFFFFFFu, x_entry = 0;
+    int64_t x_OG = 0;
+    int x_pass = 0;
 #if LZ4MI_LL_ADAPT
     const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
     unsigned int* lat = &g_lat_active[32 * xcc_id()];
@@ -1213,7 +1245,19 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     uint64_t prof_t = wall_clock64();
 #endif
 
+x_restart:
+    if (XP && xp) {
+        c.O = 0;
+        have_pf = false;
+        c.ip = x_pass ? (int32_t)x_entry
+                      : (seg_lo >= (uint32_t)c.in_len ? c.in_len : (int32_t)(seg_lo - min(seg_lo, 4096u)));
+        x_started = x_done = x_fail = false;
+        x_G = x_X = nx = x_olen = 0;
+        x_err = 0xFFFFFFFFu;
+        x_OG = 0;
+    }
     while (c.ip < c.in_len) {
+        if (XP && x_done) break;
         PROF_COUNT(10, 1);
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
         // the previous chunk's output phase, ahead of its stores) -------------
@@ -1433,13 +1477,13 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 const uint32_t k = base + g + j;
                 const int64_t os = c.O + lbase + (uint32_t)q[j].out;
                 S.t_seq[k].x = (uint32_t)os;
-                const uint32_t e = seq_error(c, os, (int64_t)c.ip + q[j].lit, q[j].ll, q[j].off, q[j].ml);
+                const uint32_t e = seq_err<XP>(c, xp, os, (int64_t)c.ip + q[j].lit, q[j].ll, q[j].off, q[j].ml);
                 if (e && first_err == 0xFFFFFFFFu) first_err = (k << 3) | e;
             }
         }
         first_err = wave_min(first_err);
         __syncthreads();
-        if (first_err != 0xFFFFFFFFu) { status = err_status(first_err & 7); break; }
+        if (first_err != 0xFFFFFFFFu && !(XP && xp)) { status = err_status(first_err & 7); break; }
 
         PROF(3);
         // ---- 6. the sequence the window could not hold: parse it from memory
@@ -1492,23 +1536,79 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             cq = q;
         }
         const int64_t tab_hi = c.O + total;
-        if (xp) {   // export: the table's sequences (output start, literal source, lengths, offset)
-            for (uint32_t k = lane; k < nseq; k += kWave) {
+        if (XP && xp) {
+            // export the sequences whose tokens lie in [seg_lo, seg_hi); the first one found is
+            // the segment's entry, the first at or past seg_hi its exit
+            const uint32_t ipc = (uint32_t)c.ip;
+            const uint32_t ntot = nseq + (cut ? 1u : 0u);   // the cut sequence is number nseq
+            const uint32_t ecut = cut ? seq_err<XP>(c, true, tab_hi, clit, cll, coff, cml) : 0u;
+            const uint32_t ferr = first_err != 0xFFFFFFFFu ? first_err : (ecut ? ((nseq << 3) | ecut) : 0xFFFFFFFFu);
+            const uint32_t fk = ferr == 0xFFFFFFFFu ? ntot : (ferr >> 3);
+            auto x_tok = [&](uint32_t k) -> uint32_t {   // token position (block-relative)
+                if (k >= nseq) return ipc + last_tok;
                 const SeqInfo q = seq_info(S, k);
-                xs[nx + k] = make_uint4((uint32_t)q.out, (uint32_t)(c.ip + q.lit), (uint32_t)q.ll,
-                                        q.ml ? (uint32_t)q.off : 0u);
+                return ipc + (uint32_t)q.lit - 1u - (q.ll >= 15 ? (uint32_t)(q.ll - 15) / 255u + 1u : 0u);
+            };
+            auto x_out = [&](uint32_t k) -> int64_t { return k >= nseq ? tab_hi : (int64_t)S.t_seq[k].x; };
+            uint32_t k0 = ntot, k1 = ntot;
+            for (uint32_t r = 0; 64u * r < ntot; ++r) {
+                const uint32_t k = 64u * r + lane;
+                const uint32_t t = k < ntot ? x_tok(k) : 0xFFFFFFFFu;
+                const uint64_t m0 = __ballot(k < ntot && t >= seg_lo), m1 = __ballot(k < ntot && t >= seg_hi);
+                if (k0 == ntot && m0) k0 = 64u * r + (uint32_t)__builtin_ctzll(m0);
+                if (k1 == ntot && m1) k1 = 64u * r + (uint32_t)__builtin_ctzll(m1);
             }
-            nx += nseq;
-            if (cut) {
-                const uint32_t e = seq_error(c, tab_hi, clit, cll, coff, cml);
-                if (e) { status = err_status(e); break; }
-                if (lane == 0) xs[nx] = make_uint4((uint32_t)tab_hi, (uint32_t)clit, (uint32_t)cll, cml ? coff : 0u);
-                ++nx;
-                c.O = tab_hi + cll + cml;
-                c.ip = (int32_t)(cq < c.in_len ? cq : c.in_len);
+            if (!x_started && fk < k0) {
+                // an error before the segment: a wrong guess, or an earlier segment's error
+                x_fail = x_done = true;
             } else {
-                c.O = tab_hi;
-                c.ip = tail >= kEnd ? c.in_len : c.ip + (int32_t)tail;
+                if (!x_started && k0 < ntot) {
+                    x_started = true;
+                    x_G = x_tok(k0);
+                    x_OG = x_out(k0);
+                }
+                if (x_started) {
+                    const uint32_t ke = fk < k1 ? fk + 1 : k1;   // with the failing one (checks 1, 4, 5)
+                    for (uint32_t k = k0 + lane; k < ke; k += kWave) {
+                        uint4 e;
+                        if (k < nseq) {
+                            const SeqInfo q = seq_info(S, k);
+                            e = make_uint4((uint32_t)(x_out(k) - x_OG), ipc + (uint32_t)q.lit, (uint32_t)q.ll,
+                                           q.ml ? (uint32_t)q.off : 0u);
+                        } else {
+                            e = make_uint4((uint32_t)(tab_hi - x_OG), (uint32_t)clit, (uint32_t)cll, cml ? coff : 0u);
+                        }
+                        xs[nx + (k - k0)] = e;
+                    }
+                    if (fk < k1) {
+                        x_err = ((nx + (fk - k0)) << 3) | (ferr & 7u);
+                        x_done = true;
+                    } else if (k1 < ntot) {
+                        x_done = true;
+                        x_X = x_tok(k1);
+                        x_olen = (uint32_t)(x_out(k1) - x_OG);
+                    }
+                    nx += ke - k0;
+                }
+            }
+            if (!x_done) {   // on to the next chunk
+                if (cut) {
+                    c.O = tab_hi + cll + cml;
+                    c.ip = (int32_t)(cq < c.in_len ? cq : c.in_len);
+                } else {
+                    c.O = tab_hi;
+                    c.ip = tail >= kEnd ? c.in_len : c.ip + (int32_t)tail;
+                }
+                if ((uint32_t)c.ip >= seg_hi && c.ip < c.in_len) {   // the chain leaps the segment's end
+                    if (!x_started) {
+                        x_started = true;
+                        x_G = (uint32_t)c.ip;
+                        x_OG = c.O;
+                    }
+                    x_done = true;
+                    x_X = (uint32_t)c.ip;
+                    x_olen = (uint32_t)(c.O - x_OG);
+                }
             }
             __syncthreads();
             continue;
@@ -1710,6 +1810,53 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         __syncthreads();
         PROF(8);
     }
+    if (XP && xp) {
+        if (!x_done) {   // the block's end
+            if (!x_started) {
+                x_G = (uint32_t)c.in_len;
+                x_OG = c.O;
+            }
+            x_X = (uint32_t)c.in_len;
+            x_olen = (uint32_t)(c.O - x_OG);
+        }
+        // the entry is right when it is the previous segment's final exit; else re-parse from
+        // that exit (pass 1, exact). Segment 0 starts at the block's first token.
+        uint32_t fin = x_err != 0xFFFFFFFFu ? kFinErr : x_X;
+        if (sg != 0 && x_pass == 0) {
+            uint32_t fp = 0;
+            if (lane == 0) {
+                const uint32_t* f = &xr[-1].fin;
+                while ((fp = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                    __builtin_amdgcn_s_sleep(8);
+            }
+            fp = lane_of(fp, 0) - 1u;
+            if (fp == kFinErr) {                       // after the block's first error: nothing here
+                nx = x_olen = 0;
+                x_err = 0xFFFFFFFFu;
+                fin = kFinErr;
+            } else if (fp >= seg_hi) {                 // the chain passes over the segment
+                nx = x_olen = 0;
+                x_err = 0xFFFFFFFFu;
+                x_G = x_X = fin = fp;
+            } else if (x_fail || fp != x_G) {
+                x_pass = 1;
+                x_entry = fp;
+                goto x_restart;
+            }
+        }
+        if (lane == 0) {
+            xr->entry = x_G;
+            xr->exit = x_X;
+            xr->cnt = nx;
+            xr->olen = x_olen;
+            xr->err = x_err;
+            __hip_atomic_store(&xr->fin, fin + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#if LZ4MI_LL_ADAPT
+        if (lat_bound && lane == 0) atomicSub(lat, 1u);
+#endif
+        return;   // status and length: lz4mi_xcheck_kernel
+    }
 #if LZ4MI_PROFILE
     if (lane == 0)
         for (int i = 0; i < 24; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
@@ -1717,7 +1864,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     if (lane == 0) {
         a.status[b] = status;
         a.out_len[b] = status ? 0u : (uint32_t)c.O;
-        if (a.xcnt) a.xcnt[b] = xp ? nx : kNotExported;
+        if (XP) a.xcnt[b] = kNotExported;   // (XP: a block past the export limits)
     }
 #if LZ4MI_LL_ADAPT
     if (lat_bound && lane == 0) atomicSub(lat, 1u);
@@ -1737,7 +1884,9 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #endif
 }
 
-__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block(a); }
+__global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block<false>(a); }
+// small batches: a wave per segment of each block, sequences exported (lz4mi_expand.hip)
+__global__ __launch_bounds__(64, 4) void lz4mi_decompress_x_kernel(DecArgs a) { decompress_block<true>(a); }
 
 // Dispatch order of a batch (LZ4MI_ORDER). Every block is one wave and a batch of up to
 // 16 blocks per CU is resident at once, so a block's decode time is its chain latency under
@@ -1833,33 +1982,45 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
 }
 
 extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, uint8_t*, const uint64_t*, const uint32_t*,
-                                          const uint8_t*, uint32_t, const uint32_t*, const int32_t*, const uint4*,
-                                          const uint32_t*, uint32_t, uint32_t*, uint32_t, uint32_t*, uint32_t,
+                                          const uint8_t*, uint32_t, uint32_t*, int32_t*, const uint4*, const uint32_t*,
+                                          lz4mi::SegRec*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*, uint32_t,
                                           hipStream_t);
 
 // A small batch in LZ4 spec mode (lz4mi_expand.hip): each block within the export limits
-// (x_in_max compressed, x_out_max output bytes) is parsed by the batch kernel, which exports
-// its sequences instead of writing them; the whole GPU then computes the output by pointer
-// jumping. Other blocks are decoded by the same launch as usual. `xs` scratch:
-// nblocks * xseq_stride sequence entries, nblocks counts, nblocks * x_out_max pointers and
-// the jump rounds' flags (lz4mi_small_scratch_bytes).
+// (x_in_max compressed, x_out_max output bytes) is parsed by kSmallSegs waves, one per segment
+// of its compressed bytes, which export its sequences instead of writing them; the whole GPU
+// then computes the output by pointer jumping. A block past the limits is decoded by the same
+// launch as usual. `xs` scratch (lz4mi_small_scratch_bytes): the segments' sequence entries,
+// the blocks' counts and segment records, nblocks * x_out_max pointers, the jump rounds' flags.
+namespace lz4mi { constexpr uint32_t kSmallSegs = 16; }
+using lz4mi::kSmallSegs;
+__host__ __device__ constexpr uint32_t small_seg_stride(uint32_t x_in_max) {
+    // a segment is at most max(4096, ceil(x_in_max / kSmallSegs) rounded up to 1 KiB) bytes;
+    // its sequences (>= 3 bytes each but the last), a failing one and the cut: L / 3 + 16
+    return (((x_in_max + kSmallSegs - 1) / kSmallSegs + 1023u) & ~1023u) / 3u + 4096u / 3u + 16u;
+}
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
-    const size_t stride = x_in_max / 3 + 8;
-    return ((size_t)nblocks * stride * 16 + 255) / 256 * 256 + ((size_t)nblocks * 4 + 255) / 256 * 256 +
-           (size_t)nblocks * x_out_max * 4 + 256;
+    const size_t seqs = (size_t)nblocks * kSmallSegs * small_seg_stride(x_in_max) * 16;
+    const size_t meta = ((size_t)nblocks * 4 + (size_t)nblocks * kSmallSegs * sizeof(lz4mi::SegRec) + 255) / 256 * 256;
+    return (seqs + 255) / 256 * 256 + meta + (size_t)nblocks * x_out_max * 4 + 256;
 }
 extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                                     const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
                                                     int32_t* status, uint32_t nblocks, uint32_t x_in_max,
                                                     uint32_t x_out_max, void* xs, hipStream_t stream) {
+    using lz4mi::SegRec;
     if (nblocks == 0) return hipSuccess;
-    const uint32_t stride = x_in_max / 3 + 8;
+    const uint32_t stride = small_seg_stride(x_in_max);
     uint8_t* p = (uint8_t*)xs;
     uint4* xseq = (uint4*)p;
-    p += ((size_t)nblocks * stride * 16 + 255) / 256 * 256;
+    p += ((size_t)nblocks * lz4mi::kSmallSegs * stride * 16 + 255) / 256 * 256;
     uint32_t* xcnt = (uint32_t*)p;
-    p += ((size_t)nblocks * 4 + 255) / 256 * 256;
+    SegRec* xrec = (SegRec*)(p + (size_t)nblocks * 4);
+    const size_t meta = ((size_t)nblocks * 4 + (size_t)nblocks * lz4mi::kSmallSegs * sizeof(SegRec) + 255) / 256 * 256;
+    hipError_t e = hipMemsetAsync(p, 0, meta, stream);   // counts (exported) and records (fin = 0: not ready)
+    if (e != hipSuccess) return e;
+    p += meta;
     uint32_t* ptr = (uint32_t*)p;
     p += (size_t)nblocks * x_out_max * 4;
     uint32_t* flags = (uint32_t*)p;
@@ -1867,12 +2028,16 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
                      nblocks > 1 ? 1 : 0, 0};
     a.xseq = xseq;
     a.xcnt = xcnt;
+    a.xrec = xrec;
     a.xseq_stride = stride;
+    a.xsegs = lz4mi::kSmallSegs;
     a.x_in_max = x_in_max;
     a.x_out_max = x_out_max;
-    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    hipError_t e = hipGetLastError();
+    // every wave of the launch is resident at once (<= 16 blocks x 16 segments): a segment's
+    // wait for the previous one's exit always ends
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, dim3(nblocks * lz4mi::kSmallSegs), dim3(64), 0, stream, a);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, stride,
-                               ptr, x_out_max, flags, nblocks, stream);
+    return lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
+                               lz4mi::kSmallSegs, stride, ptr, x_out_max, flags, nblocks, stream);
 }

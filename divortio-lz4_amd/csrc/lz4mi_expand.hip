@@ -44,10 +44,12 @@ struct ExpArgs {
     const uint32_t* out_cap;
     const uint8_t* dict;
     uint32_t dict_len;
-    const uint32_t* out_len;
-    const int32_t* status;
+    uint32_t* out_len;
+    int32_t* status;
     const uint4* xseq;
     const uint32_t* xcnt;
+    SegRec* xrec;
+    uint32_t nseg;
     uint32_t xseq_stride;
     uint32_t* ptr;            // x_out_max pointers per block
     uint32_t x_out_max;
@@ -64,43 +66,111 @@ __device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t& x0) {
     return x0 < n ? n : 0u;
 }
 
+// Per block after its segments' parse: each segment's output start, the first error in
+// sequence order (the parse's checks 2, 3 per segment; here 1, 4, 5 on every exported sequence,
+// with absolute positions: the minimum of (sequence << 3 | check) is the first check the
+// reference's decoder fails, blockDecompress.js), the block's status and length.
+__global__ __launch_bounds__(kXThreads) void lz4mi_xcheck_kernel(ExpArgs a, int isolate) {
+    const uint32_t b = blockIdx.x;
+    if (a.xcnt[b] == kNotExported) return;
+    SegRec* R = a.xrec + (size_t)b * a.nseg;
+    __shared__ uint32_t s_base[32], s_g0[32], s_best;
+    uint32_t base = 0, g = 0, stop = a.nseg, best = 0xFFFFFFFFu;
+    for (uint32_t sg = 0; sg < a.nseg; ++sg) {
+        if (threadIdx.x == 0) {
+            s_base[sg] = base;
+            s_g0[sg] = g;
+        }
+        if (R[sg].fin == kFinErr + 1u) {
+            if (R[sg].err != 0xFFFFFFFFu) best = ((g + (R[sg].err >> 3)) << 3) | (R[sg].err & 7u);
+            stop = sg + 1;
+            break;
+        }
+        base += R[sg].olen;
+        g += R[sg].cnt;
+    }
+    if (threadIdx.x == 0) s_best = best;
+    __syncthreads();
+    for (uint32_t sg = threadIdx.x; sg < stop; sg += kXThreads) R[sg].base = s_base[sg];
+    const int64_t cap = a.out_cap[b] > 0x7FFFFFFFu ? 0x7FFFFFFF : (int64_t)a.out_cap[b];
+    const int64_t out_off = (int64_t)a.out_off[b], dict_len = a.dict ? (int64_t)a.dict_len : 0;
+    uint32_t mine = 0xFFFFFFFFu;
+    for (uint32_t sg = 0; sg < stop; ++sg) {
+        const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+        const uint32_t cnt = R[sg].cnt;
+        for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
+            const uint4 e = E[k];
+            const int64_t os = (int64_t)s_base[sg] + e.x, ll = e.z, off = e.w;
+            uint32_t code = 0;
+            if (os + ll > cap) code = 1;
+            else if (off && off > out_off + os + ll + dict_len) code = 4;
+            else if (off && isolate && off > os + ll) code = 5;
+            if (code) mine = min(mine, ((s_g0[sg] + k) << 3) | code);
+        }
+    }
+    if (mine != 0xFFFFFFFFu) atomicMin(&s_best, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t e = s_best;
+        a.status[b] = e == 0xFFFFFFFFu ? 0 : ((e & 7u) == 5 ? -9 : -(int32_t)(e & 7u));
+        a.out_len[b] = e == 0xFFFFFFFFu ? base : 0u;
+    }
+}
+
 __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
     uint32_t x0;
     const uint32_t n = x_span(a, x0);
     if (!n) return;
     const uint32_t b = blockIdx.y;
-    const uint4* S = a.xseq + (size_t)b * a.xseq_stride;
-    const uint32_t cnt = a.xcnt[b];
-    // the last sequence starting at or before x0
+    const SegRec* R = a.xrec + (size_t)b * a.nseg;
+    // the segment holding x0, then its last sequence starting at or before x0
+    uint32_t sg = 0;
+    while (x0 >= R[sg].base + R[sg].olen) ++sg;
+    uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
+    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
     uint32_t lo = 0, hi = cnt;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (S[mid].x <= x0) lo = mid;
+        if (base + E[mid].x <= x0) lo = mid;
         else hi = mid;
     }
     uint32_t k = lo;
-    uint4 e = S[k];
-    uint32_t nxt = k + 1 < cnt ? S[k + 1].x : 0xFFFFFFFFu;
+    uint4 e = E[k];
+    uint32_t nxt = k + 1 < cnt ? base + E[k + 1].x : send;
     uint32_t v[kXBytes];
     bool unres = false;
 #pragma unroll
     for (int t = 0; t < kXBytes; ++t) {
         const uint32_t x = x0 + t;
-        while (x >= nxt) {
-            ++k;
-            e = S[k];
-            nxt = k + 1 < cnt ? S[k + 1].x : 0xFFFFFFFFu;
+        v[t] = 0;
+        if (x >= n) continue;
+        while (x >= nxt) {   // the next sequence (in the next non-empty segment)
+            if (k + 1 < cnt) {
+                ++k;
+            } else {
+                do {
+                    ++sg;
+                    base = R[sg].base;
+                    send = base + R[sg].olen;
+                    cnt = R[sg].cnt;
+                } while (send == base);
+                E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+                k = 0;
+            }
+            e = E[k];
+            nxt = k + 1 < cnt ? base + E[k + 1].x : send;
         }
-        if (x - e.x < e.z) {
-            v[t] = kLit | (e.y + (x - e.x));
+        const uint32_t ex = base + e.x;
+        if (x - ex < e.z) {
+            v[t] = kLit | (e.y + (x - ex));
         } else {
             // an overlapping match repeats its first `offset` bytes: point into the period
             // before the match start, so every pointer lands in an earlier sequence (a chain
             // hops at most once per sequence, not once per period)
-            const uint32_t ms = e.x + e.z, d = x - ms;
+            const uint32_t ms = ex + e.z, d = x - ms;
             const int32_t y = (int32_t)(d < e.w ? x : ms + d % e.w) - (int32_t)e.w;
             v[t] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
-            unres |= y >= 0 && x < n;
+            unres |= y >= 0;
         }
     }
     uint4* P = (uint4*)(a.ptr + (size_t)b * a.x_out_max + x0);
@@ -171,20 +241,22 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
 
 }  // namespace lz4mi
 
-// The output phase of an exported small batch: expand, up to kJumpRounds jump rounds (each
-// returns at once when the previous one left nothing to follow), gather. `flags`: scratch of
-// kJumpRounds + 1 words.
+// The output phase of an exported small batch: per-block check, expand, up to kJumpRounds jump
+// rounds (each returns at once when the previous one left nothing to follow), gather. `flags`:
+// scratch of kJumpRounds + 1 words.
 extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, uint8_t* out,
                                           const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
-                                          uint32_t dict_len, const uint32_t* out_len, const int32_t* status,
-                                          const uint4* xseq, const uint32_t* xcnt, uint32_t xseq_stride, uint32_t* ptr,
-                                          uint32_t x_out_max, uint32_t* flags, uint32_t nblocks, hipStream_t stream) {
+                                          uint32_t dict_len, uint32_t* out_len, int32_t* status, const uint4* xseq,
+                                          const uint32_t* xcnt, lz4mi::SegRec* xrec, uint32_t nseg,
+                                          uint32_t xseq_stride, uint32_t* ptr, uint32_t x_out_max, uint32_t* flags,
+                                          uint32_t nblocks, hipStream_t stream) {
     using namespace lz4mi;
     if (nblocks == 0) return hipSuccess;
-    ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xseq_stride, ptr,
-              x_out_max, flags};
+    ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
+              ptr, x_out_max, flags};
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * (kJumpRounds + 1), stream);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
     const dim3 grid((x_out_max + kXThreads * kXBytes - 1) / (kXThreads * kXBytes), nblocks);
     hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
