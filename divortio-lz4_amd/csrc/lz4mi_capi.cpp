@@ -150,15 +150,18 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
-// Small batches (at most this many blocks, LZ4 spec mode) decode by pointer jumping over the
-// whole GPU (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB block's latency
-// is then its parse, not its chain of copies. LZ4MI_SMALL_BLOCKS=0 turns it off.
+// Small batches (at most this many blocks, LZ4 spec mode) decode with 64 waves per block (a
+// segment-parallel parse) and the output by pointer jumping over the whole GPU
+// (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216 block 0.29 ms
+// instead of 7.9. Past ~60 blocks the batch kernel is faster on tiles216 (it is a flat 8.3 ms
+// up to 4096 blocks; the small path grows 0.125 ms per block), so the default is 48 blocks
+// (profiles/r05v). LZ4MI_SMALL_BLOCKS=0 turns it off.
 constexpr uint32_t kSmallInMax = (4u << 20) + (4u << 20) / 255 + 16;   // a 4 MiB block's compress bound
 constexpr uint32_t kSmallOutMax = 4u << 20;
 uint32_t small_blocks() {
     static const uint32_t n = [] {
         const char* e = std::getenv("LZ4MI_SMALL_BLOCKS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 48u;
     }();
     return n;
 }

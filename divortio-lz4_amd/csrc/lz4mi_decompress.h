@@ -32,10 +32,14 @@ struct DecArgs {
     uint32_t xseq_stride = 0;          // entries per segment
     uint32_t xsegs = 0;
     uint32_t x_in_max = 0, x_out_max = 0;
+    int xphase = 0;                    // 0: speculative parse; 1: re-parse from the first bad entry on
+    const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
+    uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)
 };
 // One segment of an exported block. Its wave parses from a guessed entry (the first token at or
-// past the segment start, found by a warm-up parse 4 KiB before it), then checks the guess
-// against the previous segment's final exit and re-parses from that exit when they differ.
+// past the segment start, found by a warm-up parse before it); lz4mi_xverify_kernel accepts the
+// segments whose entries equal their predecessors' exits, in order from segment 0 (exact), and
+// phase 1 re-parses from the first that does not (and checks the rest again, in order).
 struct SegRec {
     uint32_t entry;   // first token at or past the segment start (the chain's end: in_len)
     uint32_t exit;    // first token at or past the segment end
@@ -44,9 +48,10 @@ struct SegRec {
     uint32_t err;     // (index in the segment << 3) | check of its first parse error; 0xFFFFFFFF: none
     uint32_t fin;     // final exit + 1 once checked against the previous segment (0: not yet)
     uint32_t base;    // output start of the segment (lz4mi_xcheck_kernel)
-    uint32_t pad;
+    uint32_t fail;    // the speculative parse met an error before the segment: its guess is wrong
 };
-constexpr uint32_t kFinErr = 0xFFFFFFFEu;   // fin - 1 of a segment at or after the block's first error
+constexpr uint32_t kFinErr = 0xFFFFFFFEu;
+constexpr uint32_t kSmallSegs = 64;          // segments (waves) per exported block   // fin - 1 of a segment at or after the block's first error
 constexpr uint32_t kNotExported = 0xFFFFFFFFu;
 
 }  // namespace lz4mi

@@ -135,7 +135,9 @@ constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 256;               // longer runs are written by the whole wave (128: tiles216 +1.8 %)
 constexpr int kPeriodBulk = 1024;             // longer periodic runs are generated from an LDS copy of the pattern
-constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
+constexpr int32_t kLongLit = 4096;
+constexpr uint32_t kSegWarm = 3072;           // XP: a segment's warm-up parse (tiles216: 99 % of wrong
+                                              // starts join the token chain within 860 bytes)            // literal runs at least this long: long_literals()
 
 struct DecShared {
     union {
@@ -1225,6 +1227,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         xs = a.xseq + ((size_t)wblk * nseg + sg) * a.xseq_stride;
         xr = a.xrec + (size_t)wblk * nseg + sg;
     }
+    if (XP && a.xphase == 1 && !xp) return;
     // export state (uniform): the entry found, done, the speculation failed, entry / exit tokens,
     // sequences exported, their output bytes, the first parse error; x_OG: output position of
     // the entry in this wave's running count; pass 1: the exact re-parse from x_entry
@@ -1232,6 +1235,42 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     uint32_t x_G = 0, x_X = 0, nx = 0, x_olen = 0, x_err = 0xFFFFFFFFu, x_entry = 0;
     int64_t x_OG = 0;
     int x_pass = 0;
+    if (XP && xp && a.xphase == 1) {
+        // phase 1: segments from the first wrong entry on, in order: re-parse from the previous
+        // segment's final exit unless the speculative entry equals it
+        const uint32_t sstar = a.xfirst[wblk];
+        if (sg < sstar) return;
+        uint32_t fp = 0;
+        if (sg == sstar) {
+            fp = xr[-1].exit;                    // final: accepted by lz4mi_xverify_kernel
+        } else {
+            if (lane == 0) {
+                const uint32_t* f = &xr[-1].fin;
+                while ((fp = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                    __builtin_amdgcn_s_sleep(8);
+            }
+            fp = lane_of(fp, 0) - 1u;
+        }
+        uint32_t fin = 0;
+        bool reparse = false;
+        if (fp == kFinErr) {                     // after the block's first error: nothing here
+            fin = kFinErr;
+            if (lane == 0) { xr->cnt = 0; xr->olen = 0; xr->err = 0xFFFFFFFFu; }
+        } else if (fp >= seg_hi) {               // the chain passes over the segment
+            fin = fp;
+            if (lane == 0) { xr->entry = xr->exit = fp; xr->cnt = 0; xr->olen = 0; xr->err = 0xFFFFFFFFu; }
+        } else if (sg != sstar && !xr->fail && xr->entry == fp) {
+            fin = xr->err != 0xFFFFFFFFu ? kFinErr : xr->exit;
+        } else {
+            reparse = true;
+        }
+        if (!reparse) {
+            if (lane == 0) __hip_atomic_store(&xr->fin, fin + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        x_pass = 1;
+        x_entry = fp;
+    }
 #if LZ4MI_LL_ADAPT
     const bool lat_bound = (uint64_t)c.in_len * 2 < (uint64_t)out_cap;   // ratio > 2: a chain of short copies
     unsigned int* lat = &g_lat_active[32 * xcc_id()];
@@ -1245,19 +1284,18 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     uint64_t prof_t = wall_clock64();
 #endif
 
-x_restart:
     if (XP && xp) {
         c.O = 0;
         have_pf = false;
         c.ip = x_pass ? (int32_t)x_entry
-                      : (seg_lo >= (uint32_t)c.in_len ? c.in_len : (int32_t)(seg_lo - min(seg_lo, 4096u)));
+                      : (seg_lo >= (uint32_t)c.in_len ? c.in_len : (int32_t)(seg_lo - min(seg_lo, kSegWarm)));
         x_started = x_done = x_fail = false;
         x_G = x_X = nx = x_olen = 0;
         x_err = 0xFFFFFFFFu;
         x_OG = 0;
     }
     while (c.ip < c.in_len) {
-        if (XP && x_done) break;
+        if (XP && x_done) break;   // (XP: the segment's exit found)
         PROF_COUNT(10, 1);
         // ---- 1. stage [ip, ip + kLim) (16-byte unaligned loads, issued during
         // the previous chunk's output phase, ahead of its stores) -------------
@@ -1819,38 +1857,16 @@ x_restart:
             x_X = (uint32_t)c.in_len;
             x_olen = (uint32_t)(c.O - x_OG);
         }
-        // the entry is right when it is the previous segment's final exit; else re-parse from
-        // that exit (pass 1, exact). Segment 0 starts at the block's first token.
-        uint32_t fin = x_err != 0xFFFFFFFFu ? kFinErr : x_X;
-        if (sg != 0 && x_pass == 0) {
-            uint32_t fp = 0;
-            if (lane == 0) {
-                const uint32_t* f = &xr[-1].fin;
-                while ((fp = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
-                    __builtin_amdgcn_s_sleep(8);
-            }
-            fp = lane_of(fp, 0) - 1u;
-            if (fp == kFinErr) {                       // after the block's first error: nothing here
-                nx = x_olen = 0;
-                x_err = 0xFFFFFFFFu;
-                fin = kFinErr;
-            } else if (fp >= seg_hi) {                 // the chain passes over the segment
-                nx = x_olen = 0;
-                x_err = 0xFFFFFFFFu;
-                x_G = x_X = fin = fp;
-            } else if (x_fail || fp != x_G) {
-                x_pass = 1;
-                x_entry = fp;
-                goto x_restart;
-            }
-        }
         if (lane == 0) {
             xr->entry = x_G;
             xr->exit = x_X;
             xr->cnt = nx;
             xr->olen = x_olen;
             xr->err = x_err;
-            __hip_atomic_store(&xr->fin, fin + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            xr->fail = x_fail ? 1u : 0u;
+            if (x_pass == 1)   // the exact re-parse of phase 1: final
+                __hip_atomic_store(&xr->fin, (x_err != 0xFFFFFFFFu ? kFinErr : x_X) + 1u, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
 #if LZ4MI_LL_ADAPT
         if (lat_bound && lane == 0) atomicSub(lat, 1u);
@@ -1887,6 +1903,57 @@ x_restart:
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { decompress_block<false>(a); }
 // small batches: a wave per segment of each block, sequences exported (lz4mi_expand.hip)
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_x_kernel(DecArgs a) { decompress_block<true>(a); }
+
+// Between the two phases of an exported small batch, per block: the segments in order from
+// segment 0 (whose entry is the block's first token): each whose speculative entry equals the
+// previous one's exit is final (fin), and one the chain passes over is empty; xfirst[b] = the
+// first segment that is neither (xsegs: none), re-parsed by phase 1.
+__global__ __launch_bounds__(64) void lz4mi_xverify_kernel(DecArgs a) {
+    static_assert(kSmallSegs == 64, "one lane per segment");
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.xcnt[b] == kNotExported) return;
+    const uint32_t nseg = a.xsegs, in_len = a.in_len[b];
+    const uint32_t L = max(4096u, ((in_len + nseg - 1) / nseg + 1023u) & ~1023u);
+    SegRec* R = a.xrec + (size_t)b * nseg;
+    // the records, one per lane, in one round trip; then the walk in registers
+    const uint32_t entry = R[lane].entry, exit = R[lane].exit, err = R[lane].err, fail = R[lane].fail;
+    const uint32_t hi_l = lane + 1 == nseg ? in_len : min(in_len, lane * L + L);
+    uint32_t first = nseg, prev = 0;   // prev: the previous segment's final exit (kFinErr: an error)
+    uint32_t my_fin = 0, kind = 0;     // kind: 0 as parsed, 1 empty (after an error / passed over)
+    for (uint32_t sg = 0; sg < nseg; ++sg) {
+        const uint32_t hi = __builtin_amdgcn_readlane(hi_l, sg);
+        const uint32_t en = __builtin_amdgcn_readlane(entry, sg), ex = __builtin_amdgcn_readlane(exit, sg);
+        const uint32_t er = __builtin_amdgcn_readlane(err, sg), fl = __builtin_amdgcn_readlane(fail, sg);
+        uint32_t fin, k = 0;
+        if (sg > 0 && prev == kFinErr) {
+            fin = kFinErr;
+            k = 1;
+        } else if (sg > 0 && prev >= hi) {
+            fin = prev;
+            k = 1;
+        } else if (sg == 0 || (!fl && en == prev)) {
+            fin = er != 0xFFFFFFFFu ? kFinErr : ex;
+        } else {
+            first = sg;
+            break;
+        }
+        if (lane == sg) {
+            my_fin = fin;
+            kind = k;
+        }
+        prev = fin;
+    }
+    if (lane < first) {
+        if (kind) {   // nothing here: after the block's first error, or the chain passes over it
+            if (my_fin != kFinErr) R[lane].entry = R[lane].exit = my_fin;
+            R[lane].cnt = 0;
+            R[lane].olen = 0;
+            R[lane].err = 0xFFFFFFFFu;
+        }
+        R[lane].fin = my_fin + 1u;
+    }
+    if (lane == 0) a.xfirst_w[b] = first;
+}
 
 // Dispatch order of a batch (LZ4MI_ORDER). Every block is one wave and a batch of up to
 // 16 blocks per CU is resident at once, so a block's decode time is its chain latency under
@@ -1992,17 +2059,19 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, uint8
 // then computes the output by pointer jumping. A block past the limits is decoded by the same
 // launch as usual. `xs` scratch (lz4mi_small_scratch_bytes): the segments' sequence entries,
 // the blocks' counts and segment records, nblocks * x_out_max pointers, the jump rounds' flags.
-namespace lz4mi { constexpr uint32_t kSmallSegs = 16; }
 using lz4mi::kSmallSegs;
 __host__ __device__ constexpr uint32_t small_seg_stride(uint32_t x_in_max) {
     // a segment is at most max(4096, ceil(x_in_max / kSmallSegs) rounded up to 1 KiB) bytes;
     // its sequences (>= 3 bytes each but the last), a failing one and the cut: L / 3 + 16
     return (((x_in_max + kSmallSegs - 1) / kSmallSegs + 1023u) & ~1023u) / 3u + 4096u / 3u + 16u;
 }
+static size_t small_meta_bytes(uint32_t nblocks) {   // counts, first wrong segments, segment records
+    return ((size_t)nblocks * 8 + (size_t)nblocks * lz4mi::kSmallSegs * sizeof(lz4mi::SegRec) + 255) / 256 * 256;
+}
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
     const size_t seqs = (size_t)nblocks * kSmallSegs * small_seg_stride(x_in_max) * 16;
-    const size_t meta = ((size_t)nblocks * 4 + (size_t)nblocks * kSmallSegs * sizeof(lz4mi::SegRec) + 255) / 256 * 256;
-    return (seqs + 255) / 256 * 256 + meta + (size_t)nblocks * x_out_max * 4 + 256;
+    return (seqs + 255) / 256 * 256 + small_meta_bytes(nblocks) + (size_t)nblocks * x_out_max * 4 +
+           (size_t)nblocks * (x_out_max / 1024 + 1) * 4 + 1024;
 }
 extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -2014,30 +2083,37 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     const uint32_t stride = small_seg_stride(x_in_max);
     uint8_t* p = (uint8_t*)xs;
     uint4* xseq = (uint4*)p;
-    p += ((size_t)nblocks * lz4mi::kSmallSegs * stride * 16 + 255) / 256 * 256;
+    p += ((size_t)nblocks * kSmallSegs * stride * 16 + 255) / 256 * 256;
     uint32_t* xcnt = (uint32_t*)p;
-    SegRec* xrec = (SegRec*)(p + (size_t)nblocks * 4);
-    const size_t meta = ((size_t)nblocks * 4 + (size_t)nblocks * lz4mi::kSmallSegs * sizeof(SegRec) + 255) / 256 * 256;
-    hipError_t e = hipMemsetAsync(p, 0, meta, stream);   // counts (exported) and records (fin = 0: not ready)
+    uint32_t* xfirst = xcnt + nblocks;
+    SegRec* xrec = (SegRec*)(xfirst + nblocks);
+    hipError_t e = hipMemsetAsync(p, 0, small_meta_bytes(nblocks), stream);   // exported; records not final
     if (e != hipSuccess) return e;
-    p += meta;
+    p += small_meta_bytes(nblocks);
     uint32_t* ptr = (uint32_t*)p;
     p += (size_t)nblocks * x_out_max * 4;
-    uint32_t* flags = (uint32_t*)p;
+    uint32_t* aux = (uint32_t*)p;   // jump rounds: per-KiB done flags, then the round flags
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, 0};
     a.xseq = xseq;
     a.xcnt = xcnt;
     a.xrec = xrec;
     a.xseq_stride = stride;
-    a.xsegs = lz4mi::kSmallSegs;
+    a.xsegs = kSmallSegs;
     a.x_in_max = x_in_max;
     a.x_out_max = x_out_max;
-    // every wave of the launch is resident at once (<= 16 blocks x 16 segments): a segment's
-    // wait for the previous one's exit always ends
-    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, dim3(nblocks * lz4mi::kSmallSegs), dim3(64), 0, stream, a);
+    a.xfirst = xfirst;
+    a.xfirst_w = xfirst;
+    // phase 0: every segment speculatively; the check; phase 1: the segments from the first
+    // wrong entry on (an empty launch when there is none). Every wave of a launch is resident at
+    // once (<= 16 blocks x 64 segments), so a phase-1 wave's wait for its predecessor ends.
+    const dim3 grid(nblocks * kSmallSegs);
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    a.xphase = 1;
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     return lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
-                               lz4mi::kSmallSegs, stride, ptr, x_out_max, flags, nblocks, stream);
+                               kSmallSegs, stride, ptr, x_out_max, aux, nblocks, stream);
 }

@@ -8,7 +8,8 @@
 //   expand: every output byte x gets a source pointer: a literal byte -> its position in the
 //           compressed block (resolved), a match byte -> x - offset, an earlier output byte
 //           (unresolved) or a byte before the block (caller's history / dictionary: resolved);
-//   jump:   ptr[x] = ptr[ptr[x]] for every unresolved x, in place, round after round; each
+//   jump:   ptr[x] = ptr[ptr[x]] for every unresolved x, in place, round after round (10 rounds,
+//           then each pointer left is followed to its end: lz4mi_chase_kernel); each
 //           round at least doubles the hops a pointer has taken, so a chain of D matches is
 //           resolved in ceil(log2 D) + 1 rounds (tiles216: D <= 332, 10 rounds; text: 21 489, 16;
 //           a byte of an overlapping match points into the period before the match, so every
@@ -33,8 +34,8 @@ constexpr uint32_t kUnres = 0x80000000u;   // ptr < kUnres: an output position s
 constexpr uint32_t kLit = 0x80000000u;     // kLit | p: byte p of the compressed block
 constexpr uint32_t kHist = 0xC0000000u;    // kHist | (y + 65536): byte y < 0 before the block
 constexpr int kXThreads = 256;
-constexpr int kXBytes = 16;                // output bytes per thread
-constexpr int kJumpRounds = 21;
+constexpr int kXBytes = 16;                // output bytes per thread (a wave: 1 KiB)
+constexpr int kJumpRounds = 10;          // doubling rounds; then lz4mi_chase_kernel follows what is left
 
 struct ExpArgs {
     const uint8_t* in;
@@ -53,7 +54,9 @@ struct ExpArgs {
     uint32_t xseq_stride;
     uint32_t* ptr;            // x_out_max pointers per block
     uint32_t x_out_max;
+    uint32_t* done;           // per block and KiB of output: its pointers are all resolved
     uint32_t* flags;          // flags[r]: round r has unresolved pointers to follow
+    uint32_t* best;           // per block: min over failing sequences of (index << 3 | check)
 };
 
 // This thread's 16 output bytes [x0, x0 + 16) of block blockIdx.y, and n = the block's
@@ -65,146 +68,196 @@ __device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t& x0) {
     x0 = (blockIdx.x * kXThreads + threadIdx.x) * kXBytes;
     return x0 < n ? n : 0u;
 }
+__device__ __forceinline__ uint32_t* done_flag(const ExpArgs& a) {
+    return a.done + (size_t)blockIdx.y * (a.x_out_max / 1024) + ((blockIdx.x * kXThreads + threadIdx.x) >> 6);
+}
 
-// Per block after its segments' parse: each segment's output start, the first error in
-// sequence order (the parse's checks 2, 3 per segment; here 1, 4, 5 on every exported sequence,
-// with absolute positions: the minimum of (sequence << 3 | check) is the first check the
-// reference's decoder fails, blockDecompress.js), the block's status and length.
+// The segments before sg (all final): sg's output start and first sequence number, and
+// whether the block stopped at an error before sg (the parse's error, as its sequence code)
+__device__ __forceinline__ bool seg_prefix(const SegRec* R, uint32_t sg, uint32_t& base, uint32_t& g0, uint32_t& perr) {
+    base = g0 = 0;
+    perr = 0xFFFFFFFFu;
+    for (uint32_t s = 0; s < sg; ++s) {
+        if (R[s].fin == kFinErr + 1u) return false;
+        base += R[s].olen;
+        g0 += R[s].cnt;
+    }
+    if (R[sg].fin == kFinErr + 1u && R[sg].err != 0xFFFFFFFFu) perr = ((g0 + (R[sg].err >> 3)) << 3) | (R[sg].err & 7u);
+    return true;
+}
+
+// Per (segment, block) after the parse: the segment's output start, and the reference's checks
+// that need absolute output positions (1 capacity, 4 dictionary bounds, 5 cross-block; the parse
+// did 2 and 3) on its sequences: min of (sequence << 3 | check) over the failing ones, which is
+// the first check the reference's decoder fails (blockDecompress.js), into best[b].
 __global__ __launch_bounds__(kXThreads) void lz4mi_xcheck_kernel(ExpArgs a, int isolate) {
-    const uint32_t b = blockIdx.x;
+    const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (a.xcnt[b] == kNotExported) return;
     SegRec* R = a.xrec + (size_t)b * a.nseg;
-    __shared__ uint32_t s_base[32], s_g0[32], s_best;
-    uint32_t base = 0, g = 0, stop = a.nseg, best = 0xFFFFFFFFu;
-    for (uint32_t sg = 0; sg < a.nseg; ++sg) {
-        if (threadIdx.x == 0) {
-            s_base[sg] = base;
-            s_g0[sg] = g;
-        }
-        if (R[sg].fin == kFinErr + 1u) {
-            if (R[sg].err != 0xFFFFFFFFu) best = ((g + (R[sg].err >> 3)) << 3) | (R[sg].err & 7u);
-            stop = sg + 1;
-            break;
-        }
-        base += R[sg].olen;
-        g += R[sg].cnt;
-    }
-    if (threadIdx.x == 0) s_best = best;
-    __syncthreads();
-    for (uint32_t sg = threadIdx.x; sg < stop; sg += kXThreads) R[sg].base = s_base[sg];
+    uint32_t base, g0, perr;
+    if (!seg_prefix(R, sg, base, g0, perr)) return;   // after the block's first error
+    if (threadIdx.x == 0) R[sg].base = base;
     const int64_t cap = a.out_cap[b] > 0x7FFFFFFFu ? 0x7FFFFFFF : (int64_t)a.out_cap[b];
     const int64_t out_off = (int64_t)a.out_off[b], dict_len = a.dict ? (int64_t)a.dict_len : 0;
+    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+    const uint32_t cnt = R[sg].cnt;
     uint32_t mine = 0xFFFFFFFFu;
-    for (uint32_t sg = 0; sg < stop; ++sg) {
-        const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
-        const uint32_t cnt = R[sg].cnt;
-        for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
-            const uint4 e = E[k];
-            const int64_t os = (int64_t)s_base[sg] + e.x, ll = e.z, off = e.w;
-            uint32_t code = 0;
-            if (os + ll > cap) code = 1;
-            else if (off && off > out_off + os + ll + dict_len) code = 4;
-            else if (off && isolate && off > os + ll) code = 5;
-            if (code) mine = min(mine, ((s_g0[sg] + k) << 3) | code);
-        }
+    for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
+        const uint4 e = E[k];
+        const int64_t os = (int64_t)base + e.x, ll = e.z, off = e.w;
+        uint32_t code = 0;
+        if (os + ll > cap) code = 1;
+        else if (off && off > out_off + os + ll + dict_len) code = 4;
+        else if (off && isolate && off > os + ll) code = 5;
+        if (code) mine = min(mine, ((g0 + k) << 3) | code);
     }
-    if (mine != 0xFFFFFFFFu) atomicMin(&s_best, mine);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t e = s_best;
-        a.status[b] = e == 0xFFFFFFFFu ? 0 : ((e & 7u) == 5 ? -9 : -(int32_t)(e & 7u));
-        a.out_len[b] = e == 0xFFFFFFFFu ? base : 0u;
+    if (mine != 0xFFFFFFFFu) atomicMin(&a.best[b], mine);
+}
+
+// Per block: status and output length from the parse's first error and the checks above
+// (one lane per segment record, loaded in one round trip).
+__global__ __launch_bounds__(64) void lz4mi_xstatus_kernel(ExpArgs a) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.xcnt[b] == kNotExported) return;
+    const SegRec* R = a.xrec + (size_t)b * a.nseg;
+    const bool in = lane < a.nseg;
+    const uint32_t fin = in ? R[lane].fin : 0u, olen = in ? R[lane].olen : 0u, cnt = in ? R[lane].cnt : 0u;
+    const uint32_t err = in ? R[lane].err : 0xFFFFFFFFu;
+    const uint64_t em = __ballot(in && fin == kFinErr + 1u);
+    const uint32_t stop = em ? (uint32_t)__builtin_ctzll(em) : a.nseg;   // the first segment at an error
+    // prefix sums of the segments before `stop`
+    uint32_t base = 0, g0 = 0;
+    for (uint32_t s = 0; s < stop; ++s) {
+        base += __builtin_amdgcn_readlane(olen, s);
+        g0 += __builtin_amdgcn_readlane(cnt, s);
     }
+    if (lane != 0) return;
+    uint32_t e = a.best[b];
+    if (em) {
+        const uint32_t er = __builtin_amdgcn_readlane(err, stop);
+        if (er != 0xFFFFFFFFu) e = min(e, ((g0 + (er >> 3)) << 3) | (er & 7u));
+    }
+    a.status[b] = e == 0xFFFFFFFFu ? 0 : ((e & 7u) == 5 ? -9 : -(int32_t)(e & 7u));
+    a.out_len[b] = e == 0xFFFFFFFFu ? base : 0u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
-    uint32_t x0;
+    uint32_t x0 = 0;
     const uint32_t n = x_span(a, x0);
-    if (!n) return;
-    const uint32_t b = blockIdx.y;
-    const SegRec* R = a.xrec + (size_t)b * a.nseg;
-    // the segment holding x0, then its last sequence starting at or before x0
-    uint32_t sg = 0;
-    while (x0 >= R[sg].base + R[sg].olen) ++sg;
-    uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
-    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
-    uint32_t lo = 0, hi = cnt;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (base + E[mid].x <= x0) lo = mid;
-        else hi = mid;
-    }
-    uint32_t k = lo;
-    uint4 e = E[k];
-    uint32_t nxt = k + 1 < cnt ? base + E[k + 1].x : send;
-    uint32_t v[kXBytes];
     bool unres = false;
+    if (n) {
+        const uint32_t b = blockIdx.y;
+        const SegRec* R = a.xrec + (size_t)b * a.nseg;
+        // the segment holding x0, then its last sequence starting at or before x0
+        uint32_t sg = 0;
+        while (x0 >= R[sg].base + R[sg].olen) ++sg;
+        uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
+        const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+        uint32_t lo = 0, hi = cnt;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (base + E[mid].x <= x0) lo = mid;
+            else hi = mid;
+        }
+        uint32_t k = lo;
+        uint4 e = E[k];
+        uint32_t nxt = k + 1 < cnt ? base + E[k + 1].x : send;
+        uint32_t v[kXBytes];
 #pragma unroll
-    for (int t = 0; t < kXBytes; ++t) {
-        const uint32_t x = x0 + t;
-        v[t] = 0;
-        if (x >= n) continue;
-        while (x >= nxt) {   // the next sequence (in the next non-empty segment)
-            if (k + 1 < cnt) {
-                ++k;
-            } else {
-                do {
-                    ++sg;
-                    base = R[sg].base;
-                    send = base + R[sg].olen;
-                    cnt = R[sg].cnt;
-                } while (send == base);
-                E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
-                k = 0;
+        for (int t = 0; t < kXBytes; ++t) {
+            const uint32_t x = x0 + t;
+            v[t] = 0;
+            if (x >= n) continue;
+            while (x >= nxt) {   // the next sequence (in the next non-empty segment)
+                if (k + 1 < cnt) {
+                    ++k;
+                } else {
+                    do {
+                        ++sg;
+                        base = R[sg].base;
+                        send = base + R[sg].olen;
+                        cnt = R[sg].cnt;
+                    } while (send == base);
+                    E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+                    k = 0;
+                }
+                e = E[k];
+                nxt = k + 1 < cnt ? base + E[k + 1].x : send;
             }
-            e = E[k];
-            nxt = k + 1 < cnt ? base + E[k + 1].x : send;
+            const uint32_t ex = base + e.x;
+            if (x - ex < e.z) {
+                v[t] = kLit | (e.y + (x - ex));
+            } else {
+                // an overlapping match repeats its first `offset` bytes: point into the period
+                // before the match start, so every pointer lands in an earlier sequence (a chain
+                // hops at most once per sequence, not once per period)
+                const uint32_t ms = ex + e.z, d = x - ms;
+                const int32_t y = (int32_t)(d < e.w ? x : ms + d % e.w) - (int32_t)e.w;
+                v[t] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
+                unres |= y >= 0;
+            }
         }
-        const uint32_t ex = base + e.x;
-        if (x - ex < e.z) {
-            v[t] = kLit | (e.y + (x - ex));
-        } else {
-            // an overlapping match repeats its first `offset` bytes: point into the period
-            // before the match start, so every pointer lands in an earlier sequence (a chain
-            // hops at most once per sequence, not once per period)
-            const uint32_t ms = ex + e.z, d = x - ms;
-            const int32_t y = (int32_t)(d < e.w ? x : ms + d % e.w) - (int32_t)e.w;
-            v[t] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
-            unres |= y >= 0;
-        }
-    }
-    uint4* P = (uint4*)(a.ptr + (size_t)b * a.x_out_max + x0);
+        uint4* P = (uint4*)(a.ptr + (size_t)b * a.x_out_max + x0);
 #pragma unroll
-    for (int q = 0; q < kXBytes / 4; ++q) P[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    if (unres) a.flags[0] = 1u;
+        for (int q = 0; q < kXBytes / 4; ++q) P[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+    const uint64_t um = __ballot(unres), am = __ballot(n != 0);
+    if (am && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) *done_flag(a) = um ? 0u : 1u;
+    if (um && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) a.flags[0] = 1u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r) {
     if (a.flags[r] == 0) return;
-    uint32_t x0;
+    uint32_t x0 = 0;
     const uint32_t n = x_span(a, x0);
+    const uint64_t am = __ballot(n != 0);
+    if (!am) return;
+    uint32_t* dn = done_flag(a);
+    if (*dn) return;   // this KiB is resolved
+    bool still = false;
+    if (n) {
+        uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
+        uint4 w[kXBytes / 4];
+#pragma unroll
+        for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
+        uint32_t* v = (uint32_t*)w;
+        uint32_t u[kXBytes];
+        bool any = false;
+#pragma unroll
+        for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
+#pragma unroll
+        for (int t = 0; t < kXBytes; ++t) {
+            any |= u[t] != v[t];
+            v[t] = u[t];
+            still |= v[t] < kUnres && x0 + t < n;
+        }
+        if (any) {
+#pragma unroll
+            for (int q = 0; q < kXBytes / 4; ++q) ((uint4*)(P + x0))[q] = w[q];
+        }
+    }
+    const uint64_t sm = __ballot(still);
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) {
+        if (sm) a.flags[r + 1] = 1u;
+        else *dn = 1u;
+    }
+}
+
+// After the doubling rounds: every pointer still unresolved is followed to its end (a chain
+// deeper than 2^kJumpRounds sequences: text 21 489 -> at most 21 more hops).
+__global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
+    if (a.flags[kJumpRounds] == 0) return;
+    uint32_t x0 = 0;
+    const uint32_t n = x_span(a, x0);
+    if (__ballot(n != 0) == 0 || *done_flag(a)) return;
     if (!n) return;
     uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
-    uint4 w[kXBytes / 4];
-#pragma unroll
-    for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
-    uint32_t* v = (uint32_t*)w;
-    uint32_t u[kXBytes];
-    bool any = false;
-#pragma unroll
-    for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
-#pragma unroll
-    for (int t = 0; t < kXBytes; ++t) {
-        any |= u[t] != v[t];
-        v[t] = u[t];
+    for (int t = 0; t < kXBytes && x0 + t < n; ++t) {
+        uint32_t v = P[x0 + t];
+        if (v >= kUnres) continue;
+        while (v < kUnres) v = P[v];
+        P[x0 + t] = v;
     }
-    if (!any) return;
-#pragma unroll
-    for (int q = 0; q < kXBytes / 4; ++q) ((uint4*)(P + x0))[q] = w[q];
-    bool still = false;
-#pragma unroll
-    for (int t = 0; t < kXBytes; ++t) still |= v[t] < kUnres && x0 + t < n;
-    if (still) a.flags[r + 1] = 1u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
@@ -241,25 +294,32 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
 
 }  // namespace lz4mi
 
-// The output phase of an exported small batch: per-block check, expand, up to kJumpRounds jump
-// rounds (each returns at once when the previous one left nothing to follow), gather. `flags`:
-// scratch of kJumpRounds + 1 words.
+// The output phase of an exported small batch: the checks with absolute positions, status,
+// expand, up to kJumpRounds jump rounds (each returns at once when the previous one left
+// nothing to follow, a resolved KiB at once too), gather. `aux`: nblocks * (x_out_max / 1024)
+// done flags, then kJumpRounds + 1 round flags and nblocks check results.
 extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, uint8_t* out,
                                           const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
                                           uint32_t dict_len, uint32_t* out_len, int32_t* status, const uint4* xseq,
                                           const uint32_t* xcnt, lz4mi::SegRec* xrec, uint32_t nseg,
-                                          uint32_t xseq_stride, uint32_t* ptr, uint32_t x_out_max, uint32_t* flags,
+                                          uint32_t xseq_stride, uint32_t* ptr, uint32_t x_out_max, uint32_t* aux,
                                           uint32_t nblocks, hipStream_t stream) {
     using namespace lz4mi;
     if (nblocks == 0) return hipSuccess;
+    uint32_t* done = aux;
+    uint32_t* flags = done + (size_t)nblocks * (x_out_max / 1024);
+    uint32_t* best = flags + 32;
     ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
-              ptr, x_out_max, flags};
-    hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * (kJumpRounds + 1), stream);
+              ptr, x_out_max, done, flags, best};
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * 32, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(best, 0xFF, sizeof(uint32_t) * nblocks, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
+    hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
+    hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     const dim3 grid((x_out_max + kXThreads * kXBytes - 1) / (kXThreads * kXBytes), nblocks);
     hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
+    hipLaunchKernelGGL(lz4mi_chase_kernel, grid, dim3(kXThreads), 0, stream, a);
     hipLaunchKernelGGL(lz4mi_gather_kernel, grid, dim3(kXThreads), 0, stream, a);
     return hipGetLastError();
 }

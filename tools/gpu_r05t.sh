@@ -1,4 +1,4 @@
-# round-5 segment-parallel small-batch parse: its tests, the whole GPU suite, the small-batch
+# round-5 small-batch decode (segment-parallel parse, verify kernel, done-flag jump rounds): its tests, the whole GPU suite, the small-batch
 # latency (path on / off), and the batch kernel against the previous commit's (DecArgs grew)
 cd $GRAFT_REPO_ROOT && T=${1:-r05t} && mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
