@@ -35,6 +35,7 @@ struct DecArgs {
     int xphase = 0;                    // 0: speculative parse; 1: re-parse from the first bad entry on
     const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
     uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)
+    int xforce = 0;                    // test hook: every segment but the first counts as mis-guessed
 };
 // One segment of an exported block. Its wave parses from a guessed entry (the first token at or
 // past the segment start, found by a warm-up parse before it); lz4mi_xverify_kernel accepts the

@@ -1863,7 +1863,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             xr->cnt = nx;
             xr->olen = x_olen;
             xr->err = x_err;
-            xr->fail = x_fail ? 1u : 0u;
+            xr->fail = (x_fail || (a.xforce && sg > 0)) ? 1u : 0u;
             if (x_pass == 1)   // the exact re-parse of phase 1: final
                 __hip_atomic_store(&xr->fin, (x_err != 0xFFFFFFFFu ? kFinErr : x_X) + 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -2077,7 +2077,8 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
                                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                                     const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
                                                     int32_t* status, uint32_t nblocks, uint32_t x_in_max,
-                                                    uint32_t x_out_max, void* xs, hipStream_t stream) {
+                                                    uint32_t x_out_max, void* xs, int force_reparse,
+                                                    hipStream_t stream) {
     using lz4mi::SegRec;
     if (nblocks == 0) return hipSuccess;
     const uint32_t stride = small_seg_stride(x_in_max);
@@ -2104,6 +2105,7 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     a.x_out_max = x_out_max;
     a.xfirst = xfirst;
     a.xfirst_w = xfirst;
+    a.xforce = force_reparse;
     // phase 0: every segment speculatively; the check; phase 1: the segments from the first
     // wrong entry on (an empty launch when there is none). Every wave of a launch is resident at
     // once (<= 16 blocks x 64 segments), so a phase-1 wave's wait for its predecessor ends.

@@ -146,3 +146,50 @@ def test_small_batch_mixed_with_unexported_block():
     st, outs, lens = lz4mi.decompress_blocks(comps, [s.size for s in srcs])
     for j, s in enumerate(srcs):
         assert st[j] == 0 and lens[j] == s.size and np.array_equal(outs[j], s), j
+
+
+def _straddle_block(rng, n):
+    """Compressible data interleaved with random runs of 2-9 KiB: in the compressed block these
+    are long literal runs, so a segment's warm-up parse often starts inside one and guesses a
+    wrong entry (phase 1 re-parses it)."""
+    parts, size = [], 0
+    while size < n:
+        if rng.random() < 0.5:
+            p = rng.integers(0, 256, int(rng.integers(2048, 9216)), dtype=np.uint8)
+        else:
+            p = O.generate("tiles216", int(rng.integers(1, 10 ** 6)), int(rng.integers(4096, 40000)))
+        parts.append(p)
+        size += p.size
+    return np.concatenate(parts)[:n]
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_small_batch_segment_reparse(force, monkeypatch):
+    """Segments whose speculative entry is wrong are re-parsed from the previous segment's exit
+    (phase 1): natural mis-guesses (literal runs across segment starts) and, with the test hook
+    LZ4MI_SMALL_REPARSE, every segment past the first re-parsed in order; errors inside a
+    re-parsed segment keep the reference's first-error order."""
+    if force:
+        monkeypatch.setenv("LZ4MI_SMALL_REPARSE", "1")
+    rng = np.random.default_rng(2718)
+    srcs = [_straddle_block(rng, int(n)) for n in (4 << 20, 3 << 20, 1 << 20, 777777)]
+    srcs += [O.generate(k, 31, 2 << 20) for k in ("text", "copy", "repetitive", "random")]
+    comps = [O.compress_block_bytes(s) for s in srcs]
+    st, outs, lens = lz4mi.decompress_blocks(comps, [s.size for s in srcs])
+    for j, s in enumerate(srcs):
+        assert st[j] == 0 and lens[j] == s.size and np.array_equal(outs[j], s), (force, j)
+    bad, caps = [], []
+    for j, c in enumerate(comps):   # one corruption late in each block
+        c = c.copy()
+        c[int(c.size * 0.8) + j] ^= 0x5A
+        bad.append(c)
+        caps.append(srcs[j].size)
+    st, outs, lens = lz4mi.decompress_blocks(bad, caps)
+    for j, c in enumerate(bad):
+        est, ew, eo = O.decompress_block(c, caps[j])
+        if st[j] == lz4mi.ERR_CROSS_BLOCK:
+            assert est == lz4mi.ERR_DICT_OOB, (force, j)
+            continue
+        assert st[j] == est, (force, j, st[j], est)
+        if est == 0:
+            assert lens[j] == ew and np.array_equal(outs[j], eo[:min(ew, caps[j])]), (force, j)
