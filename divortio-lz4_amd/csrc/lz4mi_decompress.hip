@@ -2071,7 +2071,7 @@ static size_t small_meta_bytes(uint32_t nblocks) {   // counts, first wrong segm
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
     const size_t seqs = (size_t)nblocks * kSmallSegs * small_seg_stride(x_in_max) * 16;
     return (seqs + 255) / 256 * 256 + small_meta_bytes(nblocks) + (size_t)nblocks * x_out_max * 4 +
-           (size_t)nblocks * (x_out_max / 1024 + 1) * 4 + 1024;
+           128 + ((size_t)nblocks + 63) / 64 * 256 + (size_t)nblocks * (x_out_max / 16) + 256;
 }
 extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
@@ -2093,7 +2093,7 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     p += small_meta_bytes(nblocks);
     uint32_t* ptr = (uint32_t*)p;
     p += (size_t)nblocks * x_out_max * 4;
-    uint32_t* aux = (uint32_t*)p;   // jump rounds: per-KiB done flags, then the round flags
+    uint32_t* aux = (uint32_t*)p;   // jump rounds: round flags, check results, per-thread done bytes
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, 0};
     a.xseq = xseq;

@@ -54,7 +54,7 @@ struct ExpArgs {
     uint32_t xseq_stride;
     uint32_t* ptr;            // x_out_max pointers per block
     uint32_t x_out_max;
-    uint32_t* done;           // per block and KiB of output: its pointers are all resolved
+    uint8_t* done;            // per block and 16 output bytes (one thread's): its pointers are all resolved
     uint32_t* flags;          // flags[r]: round r has unresolved pointers to follow
     uint32_t* best;           // per block: min over failing sequences of (index << 3 | check)
 };
@@ -68,8 +68,8 @@ __device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t& x0) {
     x0 = (blockIdx.x * kXThreads + threadIdx.x) * kXBytes;
     return x0 < n ? n : 0u;
 }
-__device__ __forceinline__ uint32_t* done_flag(const ExpArgs& a) {
-    return a.done + (size_t)blockIdx.y * (a.x_out_max / 1024) + ((blockIdx.x * kXThreads + threadIdx.x) >> 6);
+__device__ __forceinline__ uint8_t* done_flag(const ExpArgs& a) {
+    return a.done + (size_t)blockIdx.y * (a.x_out_max / kXBytes) + blockIdx.x * kXThreads + threadIdx.x;
 }
 
 // The segments before sg (all final): sg's output start and first sequence number, and
@@ -201,46 +201,39 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
 #pragma unroll
         for (int q = 0; q < kXBytes / 4; ++q) P[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }
-    const uint64_t um = __ballot(unres), am = __ballot(n != 0);
-    if (am && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) *done_flag(a) = um ? 0u : 1u;
-    if (um && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) a.flags[0] = 1u;
+    if (n) *done_flag(a) = unres ? 0u : 1u;
+    const uint64_t um = __ballot(unres);
+    if (um && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(um)) a.flags[0] = 1u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r) {
     if (a.flags[r] == 0) return;
     uint32_t x0 = 0;
     const uint32_t n = x_span(a, x0);
-    const uint64_t am = __ballot(n != 0);
-    if (!am) return;
-    uint32_t* dn = done_flag(a);
-    if (*dn) return;   // this KiB is resolved
     bool still = false;
     if (n) {
-        uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
-        uint4 w[kXBytes / 4];
+        uint8_t* dn = done_flag(a);
+        if (*dn == 0) {   // (a resolved group skips its pointers)
+            uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
+            uint4 w[kXBytes / 4];
 #pragma unroll
-        for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
-        uint32_t* v = (uint32_t*)w;
-        uint32_t u[kXBytes];
-        bool any = false;
+            for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
+            uint32_t* v = (uint32_t*)w;
+            uint32_t u[kXBytes];
 #pragma unroll
-        for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
+            for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
 #pragma unroll
-        for (int t = 0; t < kXBytes; ++t) {
-            any |= u[t] != v[t];
-            v[t] = u[t];
-            still |= v[t] < kUnres && x0 + t < n;
-        }
-        if (any) {
+            for (int t = 0; t < kXBytes; ++t) {
+                v[t] = u[t];
+                still |= v[t] < kUnres && x0 + t < n;
+            }
 #pragma unroll
             for (int q = 0; q < kXBytes / 4; ++q) ((uint4*)(P + x0))[q] = w[q];
+            if (!still) *dn = 1u;
         }
     }
     const uint64_t sm = __ballot(still);
-    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(am)) {
-        if (sm) a.flags[r + 1] = 1u;
-        else *dn = 1u;
-    }
+    if (sm && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(sm)) a.flags[r + 1] = 1u;
 }
 
 // After the doubling rounds: every pointer still unresolved is followed to its end (a chain
@@ -249,8 +242,7 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
     if (a.flags[kJumpRounds] == 0) return;
     uint32_t x0 = 0;
     const uint32_t n = x_span(a, x0);
-    if (__ballot(n != 0) == 0 || *done_flag(a)) return;
-    if (!n) return;
+    if (!n || *done_flag(a)) return;
     uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
     for (int t = 0; t < kXBytes && x0 + t < n; ++t) {
         uint32_t v = P[x0 + t];
@@ -296,8 +288,8 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
 
 // The output phase of an exported small batch: the checks with absolute positions, status,
 // expand, up to kJumpRounds jump rounds (each returns at once when the previous one left
-// nothing to follow, a resolved KiB at once too), gather. `aux`: nblocks * (x_out_max / 1024)
-// done flags, then kJumpRounds + 1 round flags and nblocks check results.
+// nothing to follow; a thread whose 16 bytes are resolved at once too), gather. `aux`: the round
+// flags (32 words), nblocks check results, then nblocks * x_out_max / 16 done bytes.
 extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, uint8_t* out,
                                           const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
                                           uint32_t dict_len, uint32_t* out_len, int32_t* status, const uint4* xseq,
@@ -306,9 +298,9 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
                                           uint32_t nblocks, hipStream_t stream) {
     using namespace lz4mi;
     if (nblocks == 0) return hipSuccess;
-    uint32_t* done = aux;
-    uint32_t* flags = done + (size_t)nblocks * (x_out_max / 1024);
+    uint32_t* flags = aux;
     uint32_t* best = flags + 32;
+    uint8_t* done = (uint8_t*)(best + ((nblocks + 63) & ~63u));
     ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
               ptr, x_out_max, done, flags, best};
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * 32, stream);
