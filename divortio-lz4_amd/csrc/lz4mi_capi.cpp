@@ -28,7 +28,7 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t*, const uint64_t*, c
 extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                     const uint64_t*, const uint32_t*, const uint8_t*, uint32_t,
                                                     uint32_t*, int32_t*, uint32_t, uint32_t, uint32_t, void*, int,
-                                                    hipStream_t);
+                                                    int, hipStream_t);
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t, uint32_t, uint32_t);
 extern "C" hipError_t lz4mi_launch_compress(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                             const uint64_t*, uint32_t*, uint32_t, int32_t*, hipStream_t);
@@ -174,11 +174,12 @@ hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
                          Scratch* order, Scratch* small = nullptr) {
-    if (small && mode == 0 && nblocks <= small_blocks() &&
+    if (small && (mode == 0 || mode == 2) && nblocks <= small_blocks() &&
         small->ensure(lz4mi_small_scratch_bytes(nblocks, kSmallInMax, kSmallOutMax), s) == hipSuccess)
         return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
                                              status, nblocks, kSmallInMax, kSmallOutMax, small->p,
-                                             std::getenv("LZ4MI_SMALL_REPARSE") ? 1 : 0, s);   // (test hook)
+                                             std::getenv("LZ4MI_SMALL_REPARSE") ? 1 : 0,   // (test hook)
+                                             mode == 2 ? 1 : 0, s);
     uint32_t* ord = nullptr;
     if (order && nblocks > 1 && order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,

@@ -36,6 +36,7 @@ struct DecArgs {
     const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
     uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)
     int xforce = 0;                    // test hook: every segment but the first counts as mis-guessed
+    const uint32_t* redo = nullptr;    // batch kernel: decode only the blocks with redo[b] != 0 (nullptr: all)
 };
 // One segment of an exported block. Its wave parses from a guessed entry (the first token at or
 // past the segment start, found by a warm-up parse before it); lz4mi_xverify_kernel accepts the

@@ -1176,6 +1176,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const uint32_t wblk = XP ? blockIdx.x / nseg : blockIdx.x;
     const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;
     const uint32_t b = a.order ? uniform(a.order[wblk]) : wblk;
+    if (!XP && a.redo && !uniform(a.redo[b])) return;   // (small batches, reference mode: the blocks to redo)
 #if LZ4MI_TIMELINE
     const uint64_t tl_t0 = wall_clock64();
 #endif
@@ -2050,8 +2051,8 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
 
 extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, uint8_t*, const uint64_t*, const uint32_t*,
                                           const uint8_t*, uint32_t, uint32_t*, int32_t*, const uint4*, const uint32_t*,
-                                          lz4mi::SegRec*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*, uint32_t,
-                                          hipStream_t);
+                                          lz4mi::SegRec*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*, int,
+                                          uint32_t**, uint32_t, hipStream_t);
 
 // A small batch in LZ4 spec mode (lz4mi_expand.hip): each block within the export limits
 // (x_in_max compressed, x_out_max output bytes) is parsed by kSmallSegs waves, one per segment
@@ -2071,13 +2072,13 @@ static size_t small_meta_bytes(uint32_t nblocks) {   // counts, first wrong segm
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
     const size_t seqs = (size_t)nblocks * kSmallSegs * small_seg_stride(x_in_max) * 16;
     return (seqs + 255) / 256 * 256 + small_meta_bytes(nblocks) + (size_t)nblocks * x_out_max * 4 +
-           128 + ((size_t)nblocks + 63) / 64 * 256 + (size_t)nblocks * (x_out_max / 16) + 256;
+           128 + ((size_t)nblocks + 63) / 64 * 512 + (size_t)nblocks * (x_out_max / 16) + 256;
 }
 extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                                     uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                                     const uint8_t* dict, uint32_t dict_len, uint32_t* out_len,
                                                     int32_t* status, uint32_t nblocks, uint32_t x_in_max,
-                                                    uint32_t x_out_max, void* xs, int force_reparse,
+                                                    uint32_t x_out_max, void* xs, int force_reparse, int f1,
                                                     hipStream_t stream) {
     using lz4mi::SegRec;
     if (nblocks == 0) return hipSuccess;
@@ -2116,6 +2117,16 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
-                               kSmallSegs, stride, ptr, x_out_max, aux, nblocks, stream);
+    uint32_t* redo = nullptr;
+    e = lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
+                            kSmallSegs, stride, ptr, x_out_max, aux, f1, &redo, nblocks, stream);
+    if (e != hipSuccess || !f1) return e;
+    // reference mode (LZ4MI_JS_EXACT): the blocks whose output a double-copy-tail rewrite would
+    // change (lz4mi_xf1_kernel) are decoded again by the batch kernel's in-chunk fix-up; the
+    // launch is empty when there are none
+    lz4mi::DecArgs r{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
+                     nblocks > 1 ? 1 : 0, 1};
+    r.redo = redo;
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_kernel, dim3(nblocks), dim3(64), 0, stream, r);
+    return hipGetLastError();
 }

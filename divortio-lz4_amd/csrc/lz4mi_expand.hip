@@ -252,6 +252,37 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
     }
 }
 
+// Reference mode (LZ4MI_JS_EXACT): would the reference's double-copy-tail rewrite
+// (blockDecompress.js:219-250, SURVEY.md F1: offset >= 8, length < 8) change a byte of the
+// finished output? The spec output is the reference's exactly when no rewrite changes a byte (a
+// rewrite reads bytes before its match, final by then, that no later rewrite touches); a block
+// with one is decoded again by the batch kernel's fix-up (redo[b]). One workgroup per segment.
+__global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int isolate, uint32_t* redo) {
+    const uint32_t sg = blockIdx.x, b = blockIdx.y;
+    if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return;
+    const SegRec* R = a.xrec + (size_t)b * a.nseg;
+    const uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
+    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+    const int64_t out_off = (int64_t)a.out_off[b];
+    const int64_t cap = min(a.out_len[b], a.out_cap[b]);
+    const uint8_t* dst = a.out + out_off;
+    bool ch = false;
+    for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
+        const uint4 e = E[k];
+        const int64_t ms = (int64_t)base + e.x + e.z, off = e.w;
+        const int64_t ml = (k + 1 < cnt ? (int64_t)base + E[k + 1].x : (int64_t)send) - ms;
+        if (ml == 0 || ml >= 8 || off < 8 || out_off + ms - off < 0) continue;
+        const int64_t p0 = ms + ml - 8;
+        if (p0 - off < 0) {
+            ch = true;   // (batched: reported as LZ4MI_ERR_CROSS_BLOCK by the redo)
+            continue;
+        }
+        for (int64_t q = p0; q < ms && q < cap; ++q) ch |= dst[q] != dst[q - off];
+    }
+    (void)isolate;
+    if (ch) redo[b] = 1u;
+}
+
 __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
     uint32_t x0;
     const uint32_t n = x_span(a, x0);
@@ -295,16 +326,19 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
                                           uint32_t dict_len, uint32_t* out_len, int32_t* status, const uint4* xseq,
                                           const uint32_t* xcnt, lz4mi::SegRec* xrec, uint32_t nseg,
                                           uint32_t xseq_stride, uint32_t* ptr, uint32_t x_out_max, uint32_t* aux,
-                                          uint32_t nblocks, hipStream_t stream) {
+                                          int f1, uint32_t** redo_out, uint32_t nblocks, hipStream_t stream) {
     using namespace lz4mi;
     if (nblocks == 0) return hipSuccess;
     uint32_t* flags = aux;
     uint32_t* best = flags + 32;
-    uint8_t* done = (uint8_t*)(best + ((nblocks + 63) & ~63u));
+    uint32_t* redo = best + ((nblocks + 63) & ~63u);
+    uint8_t* done = (uint8_t*)(redo + ((nblocks + 63) & ~63u));
+    *redo_out = redo;
     ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
               ptr, x_out_max, done, flags, best};
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * 32, stream);
     if (e == hipSuccess) e = hipMemsetAsync(best, 0xFF, sizeof(uint32_t) * nblocks, stream);
+    if (e == hipSuccess && f1) e = hipMemsetAsync(redo, 0, sizeof(uint32_t) * nblocks, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
     hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
@@ -313,5 +347,8 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
     hipLaunchKernelGGL(lz4mi_chase_kernel, grid, dim3(kXThreads), 0, stream, a);
     hipLaunchKernelGGL(lz4mi_gather_kernel, grid, dim3(kXThreads), 0, stream, a);
+    if (f1)
+        hipLaunchKernelGGL(lz4mi_xf1_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0,
+                           redo);
     return hipGetLastError();
 }

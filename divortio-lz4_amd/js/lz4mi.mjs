@@ -80,16 +80,20 @@ function blockId(bytes) {             // bufferCompress.js:77-82
     return 7;
 }
 
-// Routing (SURVEY.md §8b, DESIGN §5.1). A batch of b independent blocks costs the GPU about
-// one block's chain latency (every block is one wave, all resident at once) plus the PCIe
-// copies, and the host b blocks one after another, so the GPU wins from a block count on that
-// is nearly independent of the block size. The crossovers below are measured on the box
+// Routing (SURVEY.md §8b, DESIGN §5.1). A compress batch of b independent blocks costs the GPU
+// about one block's chain latency (every block is one wave, all resident at once) plus the
+// PCIe copies, and the host b blocks one after another, so the GPU wins from a block count on
+// that is nearly independent of the block size. The crossovers below are measured on the box
 // (bench.py `single_block` and `napi_end_to_end.crossover`; 4 MiB tiles216: compress GPU
-// ~31 ms for one block vs host 1.1 ms per block, decode GPU ~8-12 ms + 0.09 ms per block vs
-// host 0.23 ms per block). A raw-block call is one block: the host's. 'gpu' / 'host' force
-// one side for every call (tests, and measuring the crossover).
+// ~29 ms for one block vs host 1.1 ms per block -> 32 blocks). Decode of up to 48 blocks takes
+// the small-batch path (64 waves per block, round 5): through N-API 0.41 ms per block + ~2.8 ms
+// against the host's ~1 ms per block (4 blocks 4.5 vs 3.8 ms, 16 blocks 9.4 vs 15.6), a
+// crossover at ~5 blocks; 8 keeps frames of a few blocks whose reference-mode decode needs the
+// double-copy-tail fix-up (the reference's own 25 MiB JSON benchmark: 7 blocks) on the host.
+// A raw-block call is one block: the host's. 'gpu' / 'host' force one side for every call
+// (tests, and measuring the crossover).
 const HOST_MAX_BLOCKS_COMPRESS = 32;
-const HOST_MAX_BLOCKS_DECOMPRESS = 64;
+const HOST_MAX_BLOCKS_DECOMPRESS = 8;
 let routing = 'auto';
 
 /** 'auto' (default: the measured crossovers above), 'gpu' or 'host' (every block call on that side). */

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--gens", default="tiles216,text,repetitive")
     ap.add_argument("--counts", default="1,2,4,8,16")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--js-exact", action="store_true", help="reference mode (LZ4MI_JS_EXACT)")
     args = ap.parse_args()
     import torch
     import lz4mi
@@ -28,7 +29,8 @@ def main():
     torch.cuda.set_stream(s)
     sp = s.cuda_stream
     n = max(int(x) for x in args.counts.split(","))
-    res = {"small_blocks_env": os.environ.get("LZ4MI_SMALL_BLOCKS", "default")}
+    flags = 1 | (8 if args.js_exact else 0)   # LZ4MI_DEVICE_PTRS | LZ4MI_JS_EXACT
+    res = {"small_blocks_env": os.environ.get("LZ4MI_SMALL_BLOCKS", "default"), "js_exact": args.js_exact}
     for gen in args.gens.split(","):
         raw = make_raw(torch, lz4mi, gen, n, sp)
         slot = (lz4mi.compress_bound(BLOCK) + 255) & ~255
@@ -45,8 +47,10 @@ def main():
         row = {}
         for b in (int(x) for x in args.counts.split(",")):
             def run():
-                lz4mi.decompress_blocks_dev(comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), dec.data_ptr(),
-                                            roff.data_ptr(), rlen.data_ptr(), dlen.data_ptr(), st.data_ptr(), b, sp)
+                r = lz4mi.lib().lz4mi_decompress_blocks(comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), dec.data_ptr(),
+                                                        roff.data_ptr(), rlen.data_ptr(), None, 0, dlen.data_ptr(),
+                                                        st.data_ptr(), b, flags, sp)
+                assert r == 0
             run()
             torch.cuda.synchronize()
             ts = []
