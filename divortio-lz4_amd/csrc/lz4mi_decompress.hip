@@ -2095,8 +2095,9 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     uint32_t* ptr = (uint32_t*)p;
     p += (size_t)nblocks * x_out_max * 4;
     uint32_t* aux = (uint32_t*)p;   // jump rounds: round flags, check results, per-thread done bytes
+    // (f1check: a block past the export limits is decoded by its segment-0 wave in the caller's mode)
     lz4mi::DecArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
-                     nblocks > 1 ? 1 : 0, 0};
+                     nblocks > 1 ? 1 : 0, f1};
     a.xseq = xseq;
     a.xcnt = xcnt;
     a.xrec = xrec;

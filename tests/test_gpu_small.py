@@ -193,3 +193,23 @@ def test_small_batch_segment_reparse(force, monkeypatch):
         assert st[j] == est, (force, j, st[j], est)
         if est == 0:
             assert lens[j] == ew and np.array_equal(outs[j], eo[:min(ew, caps[j])]), (force, j)
+
+
+def test_small_batch_reference_mode_matches_reference_decoder():
+    """Reference mode (LZ4MI_JS_EXACT) through the small path: blocks whose output a
+    double-copy-tail rewrite changes are decoded again by the batch kernel's fix-up,
+    a block past the export limit is decoded in reference mode by the same launch; every result
+    equals the reference-exact oracle decode (oracle js_compat), alone and batched."""
+    srcs = [O.generate("copy", 61, 1 << 20), O.generate("tiles216", 62, 1 << 20),
+            O.generate("copy", 63, (4 << 20) + 4096), O.generate("runs", 64, 700000), O.generate("text", 65, 300000)]
+    comps = [O.compress_block_bytes(s) for s in srcs]
+    for sel in ([0], [1], [2], [0, 1, 2, 3, 4]):
+        st, outs, lens = lz4mi.decompress_blocks([comps[i] for i in sel], [srcs[i].size for i in sel], js_exact=True)
+        for j, i in enumerate(sel):
+            est, ew, eo = O.decompress_block(comps[i], srcs[i].size, js_compat=True)
+            if st[j] == lz4mi.ERR_CROSS_BLOCK:     # batched: the rewrite reaches before the block
+                assert len(sel) > 1, (sel, i)
+                continue
+            assert st[j] == est and lens[j] == ew, (sel, i, st[j], est)
+            if est == 0:
+                assert np.array_equal(outs[j], eo[:ew]), (sel, i)
