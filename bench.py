@@ -607,6 +607,12 @@ def main():
                         "compress_GBps": round(nb * BLOCK / ck / 1e9, 2),
                         "roundtrip_GBps": round(nb * BLOCK / (ck + k) / 1e9, 2),
                         "verified": b2.verify(torch, lz4mi, stream)}
+            # the batch's first block alone (the small-batch decode path)
+            _, k1 = timed(torch, None, lambda: lz4mi.decompress_blocks_dev(
+                b2.comp.data_ptr(), b2.comp_off.data_ptr(), b2.comp_len.data_ptr(), b2.dec.data_ptr(),
+                b2.raw_off.data_ptr(), b2.raw_len.data_ptr(), b2.dec_len.data_ptr(), b2.status.data_ptr(), 1,
+                stream), 3, 1, stream_obj)
+            extra[g]["lone_block_decompress_ms"] = round(k1 * 1e3, 3)
             del b2
             torch.cuda.empty_cache()
         batch.dec = torch.empty(1, dtype=torch.uint8, device="cuda")
