@@ -151,18 +151,19 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
-// Small batches (at most this many blocks, LZ4 spec mode) decode with 64 waves per block (a
-// segment-parallel parse) and the output by pointer jumping over the whole GPU
-// (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216 block 0.29 ms
-// instead of 7.9. Past ~60 blocks the batch kernel is faster on tiles216 (it is a flat 8.3 ms
-// up to 4096 blocks; the small path grows 0.125 ms per block), so the default is 48 blocks
-// (profiles/r05v). LZ4MI_SMALL_BLOCKS=0 turns it off.
+// Small batches (at most this many blocks, LZ4 spec or reference mode) decode with 64 waves per
+// block (a segment-parallel parse) and the output by pointer jumping over the whole GPU
+// (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216 block 0.25 ms instead
+// of 7.9. The batch kernel is a flat 8.3 ms up to 4096 tiles216 blocks; the small path grows
+// ~0.063 ms per block (128 blocks: 8.13 ms, profiles/r06c), so the default is 96 blocks. Blocks
+// of long runs (ratio >= 32) are decoded by one wave in the same launch. LZ4MI_SMALL_BLOCKS=0
+// turns the path off.
 constexpr uint32_t kSmallInMax = (4u << 20) + (4u << 20) / 255 + 16;   // a 4 MiB block's compress bound
 constexpr uint32_t kSmallOutMax = 4u << 20;
 uint32_t small_blocks() {
     static const uint32_t n = [] {
         const char* e = std::getenv("LZ4MI_SMALL_BLOCKS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 48u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 96u;
     }();
     return n;
 }

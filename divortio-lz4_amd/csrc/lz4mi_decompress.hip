@@ -136,6 +136,7 @@ constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: 
 constexpr int kLaneBytes = 256;               // longer runs are written by the whole wave (128: tiles216 +1.8 %)
 constexpr int kPeriodBulk = 1024;             // longer periodic runs are generated from an LDS copy of the pattern
 constexpr int32_t kLongLit = 4096;
+constexpr uint64_t kXRatioMax = 32;           // XP: blocks of higher ratio are decoded by one wave
 constexpr uint32_t kSegWarm = 3072;           // XP: a segment's warm-up parse (tiles216: 99 % of wrong
                                               // starts join the token chain within 860 bytes)            // literal runs at least this long: long_literals()
 
@@ -1173,8 +1174,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const int lane = threadIdx.x;
     const uint32_t nseg = XP ? a.xsegs : 1u;   // XP: waves per block (one per segment)
     if (blockIdx.x >= a.nblocks * nseg) return;
-    const uint32_t wblk = XP ? blockIdx.x / nseg : blockIdx.x;
-    const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;
+    const uint32_t wblk = XP ? blockIdx.x / nseg : blockIdx.x;   // (XP: block-major, segments of a block on
+    const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;       //  64 consecutive CUs, every XCD)
     const uint32_t b = a.order ? uniform(a.order[wblk]) : wblk;
     if (!XP && a.redo && !uniform(a.redo[b])) return;   // (small batches, reference mode: the blocks to redo)
 #if LZ4MI_TIMELINE
@@ -1216,8 +1217,15 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
         return;
     }
     // small-batch export (XP, lz4mi_expand.hip): segment sg of the block, parsed only
-    const bool xp = XP && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max;
-    if (XP && !xp && sg != 0) return;   // past the export limits: its segment-0 wave decodes it as usual
+    // (a block of long runs -- output over 32x its compressed size: repetitive data, one periodic
+    // match -- decodes faster in one wave, as in the batch kernel: 1.1 ms for 4 MiB at any batch
+    // size, against 0.77 ms alone / 1.57 ms for 16 through the pointers, profiles/r06c)
+    const bool xp = XP && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max &&
+                    (uint64_t)out_cap < (uint64_t)c.in_len * kXRatioMax;
+    // past the export limits (or ratio >= 32): one wave decodes the block as usual -- segment
+    // b mod 64, i.e. workgroup 65 b (mod 256 CUs: a CU of its own for every block, where
+    // segment 0 would put the blocks of a batch on 4 CUs)
+    if (XP && !xp && sg != wblk % nseg) return;
     uint4* xs = nullptr;
     SegRec* xr = nullptr;
     uint32_t seg_lo = 0, seg_hi = 0;    // the segment: tokens in [seg_lo, seg_hi)

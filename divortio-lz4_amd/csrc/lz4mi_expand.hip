@@ -57,19 +57,27 @@ struct ExpArgs {
     uint8_t* done;            // per block and 16 output bytes (one thread's): its pointers are all resolved
     uint32_t* flags;          // flags[r]: round r has unresolved pointers to follow
     uint32_t* best;           // per block: min over failing sequences of (index << 3 | check)
+    uint32_t ntiles;          // nblocks * x_out_max / kTile
+    uint32_t tshift;          // log2(x_out_max / kTile)
 };
 
-// This thread's 16 output bytes [x0, x0 + 16) of block blockIdx.y, and n = the block's
+// The output kernels loop over (block, tile) pairs, a tile = kXThreads * kXBytes output bytes,
+// with a grid of at most kXGrid workgroups (one tile each up to 128 blocks of 4 MiB).
+constexpr uint32_t kTile = kXThreads * kXBytes;
+constexpr uint32_t kXGrid = 1u << 17;   // (2048: 8-10 % slower on tiles216, profiles/r06e)
+#define X_TILES(a) for (uint32_t tile_ = blockIdx.x; tile_ < (a).ntiles; tile_ += gridDim.x)
+#define X_B(a) (tile_ >> (a).tshift)                  // (x_out_max / kTile: a power of two)
+#define X_T(a) (tile_ & ((1u << (a).tshift) - 1u))
+// This thread's 16 output bytes [x0, x0 + 16) of tile t of block b, and n = the block's
 // output length (0: nothing to do here)
-__device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t& x0) {
-    const uint32_t b = blockIdx.y;
+__device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t b, uint32_t t, uint32_t& x0) {
     if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return 0;
     const uint32_t n = min(a.out_len[b], a.out_cap[b]);
-    x0 = (blockIdx.x * kXThreads + threadIdx.x) * kXBytes;
+    x0 = t * kTile + threadIdx.x * kXBytes;
     return x0 < n ? n : 0u;
 }
-__device__ __forceinline__ uint8_t* done_flag(const ExpArgs& a) {
-    return a.done + (size_t)blockIdx.y * (a.x_out_max / kXBytes) + blockIdx.x * kXThreads + threadIdx.x;
+__device__ __forceinline__ uint8_t* done_flag(const ExpArgs& a, uint32_t b, uint32_t t) {
+    return a.done + (size_t)b * (a.x_out_max / kXBytes) + t * kXThreads + threadIdx.x;
 }
 
 // The segments before sg (all final): sg's output start and first sequence number, and
@@ -142,11 +150,12 @@ __global__ __launch_bounds__(64) void lz4mi_xstatus_kernel(ExpArgs a) {
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
+  bool unres = false;
+  X_TILES(a) {
     uint32_t x0 = 0;
-    const uint32_t n = x_span(a, x0);
-    bool unres = false;
+    const uint32_t b = X_B(a);
+    const uint32_t n = x_span(a, b, X_T(a), x0);
     if (n) {
-        const uint32_t b = blockIdx.y;
         const SegRec* R = a.xrec + (size_t)b * a.nseg;
         // the segment holding x0, then its last sequence starting at or before x0
         uint32_t sg = 0;
@@ -201,37 +210,51 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
 #pragma unroll
         for (int q = 0; q < kXBytes / 4; ++q) P[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }
-    if (n) *done_flag(a) = unres ? 0u : 1u;
+  }
     const uint64_t um = __ballot(unres);
     if (um && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(um)) a.flags[0] = 1u;
 }
 
+// The jump rounds and the chase work on a wave's KiB of output strided: lane l holds bytes
+// l, l + 64, ... l + 960, so each load, gather and store instruction of the wave covers 256
+// contiguous bytes (2 cache lines) and the gathers follow runs of consecutive sources -- with
+// 16 consecutive bytes per lane an instruction spans 4 KiB (32 lines). done[]: per lane, its
+// 16 bytes are resolved (zeroed before the first round).
+__device__ __forceinline__ uint32_t x_wave(const ExpArgs& a, uint32_t b, uint32_t t, uint32_t& wbase) {
+    if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return 0;
+    const uint32_t n = min(a.out_len[b], a.out_cap[b]);
+    wbase = t * kTile + (threadIdx.x >> 6) * (64 * kXBytes);
+    return wbase < n ? n : 0u;
+}
+
 __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r) {
-    if (a.flags[r] == 0) return;
-    uint32_t x0 = 0;
-    const uint32_t n = x_span(a, x0);
-    bool still = false;
-    if (n) {
-        uint8_t* dn = done_flag(a);
-        if (*dn == 0) {   // (a resolved group skips its pointers)
-            uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
-            uint4 w[kXBytes / 4];
+  if (a.flags[r] == 0) return;
+  bool still = false;
+  X_TILES(a) {
+    uint32_t wbase = 0;
+    const uint32_t b = X_B(a), t = X_T(a);
+    const uint32_t n = x_wave(a, b, t, wbase);
+    if (!n) continue;
+    const uint32_t lane = threadIdx.x & 63;
+    uint8_t* dn = done_flag(a, b, t);
+    bool mine = false;
+    if (*dn == 0) {
+        uint32_t* P = a.ptr + (size_t)b * a.x_out_max + wbase + lane;
+        const uint32_t* Q = a.ptr + (size_t)b * a.x_out_max;
+        uint32_t v[kXBytes];
 #pragma unroll
-            for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)(P + x0))[q];
-            uint32_t* v = (uint32_t*)w;
-            uint32_t u[kXBytes];
+        for (int k = 0; k < kXBytes; ++k) v[k] = wbase + lane + 64 * k < n ? P[64 * k] : kLit;
 #pragma unroll
-            for (int t = 0; t < kXBytes; ++t) u[t] = (v[t] < kUnres && x0 + t < n) ? P[v[t]] : v[t];
+        for (int k = 0; k < kXBytes; ++k) v[k] = v[k] < kUnres ? Q[v[k]] : v[k];
 #pragma unroll
-            for (int t = 0; t < kXBytes; ++t) {
-                v[t] = u[t];
-                still |= v[t] < kUnres && x0 + t < n;
-            }
-#pragma unroll
-            for (int q = 0; q < kXBytes / 4; ++q) ((uint4*)(P + x0))[q] = w[q];
-            if (!still) *dn = 1u;
+        for (int k = 0; k < kXBytes; ++k) {
+            if (wbase + lane + 64 * k < n) P[64 * k] = v[k];
+            mine |= v[k] < kUnres;
         }
+        if (!mine) *dn = 1u;
     }
+    still |= mine;
+  }
     const uint64_t sm = __ballot(still);
     if (sm && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(sm)) a.flags[r + 1] = 1u;
 }
@@ -239,17 +262,23 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r)
 // After the doubling rounds: every pointer still unresolved is followed to its end (a chain
 // deeper than 2^kJumpRounds sequences: text 21 489 -> at most 21 more hops).
 __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
-    if (a.flags[kJumpRounds] == 0) return;
-    uint32_t x0 = 0;
-    const uint32_t n = x_span(a, x0);
-    if (!n || *done_flag(a)) return;
-    uint32_t* P = a.ptr + (size_t)blockIdx.y * a.x_out_max;
-    for (int t = 0; t < kXBytes && x0 + t < n; ++t) {
-        uint32_t v = P[x0 + t];
+  if (a.flags[kJumpRounds] == 0) return;
+  X_TILES(a) {
+    uint32_t wbase = 0;
+    const uint32_t b = X_B(a), t = X_T(a);
+    const uint32_t n = x_wave(a, b, t, wbase);
+    if (!n || *done_flag(a, b, t)) continue;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* Q = a.ptr + (size_t)b * a.x_out_max;
+    for (int k = 0; k < kXBytes; ++k) {
+        const uint32_t x = wbase + lane + 64 * k;
+        if (x >= n) break;
+        uint32_t v = Q[x];
         if (v >= kUnres) continue;
-        while (v < kUnres) v = P[v];
-        P[x0 + t] = v;
+        while (v < kUnres) v = Q[v];
+        Q[x] = v;
     }
+  }
 }
 
 // Reference mode (LZ4MI_JS_EXACT): would the reference's double-copy-tail rewrite
@@ -284,10 +313,11 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int iso
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
+  X_TILES(a) {
     uint32_t x0;
-    const uint32_t n = x_span(a, x0);
-    if (!n) return;
-    const uint32_t b = blockIdx.y;
+    const uint32_t b = X_B(a);
+    const uint32_t n = x_span(a, b, X_T(a), x0);
+    if (!n) continue;
     const uint32_t* P = a.ptr + (size_t)b * a.x_out_max + x0;
     const uint8_t* src = a.in + a.in_off[b];
     uint8_t* dst = a.out + a.out_off[b];
@@ -313,6 +343,7 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
     } else {
         for (uint32_t t = 0; x0 + t < n; ++t) dst[x0 + t] = (uint8_t)(o[t >> 2] >> (8 * (t & 3)));
     }
+  }
 }
 
 }  // namespace lz4mi
@@ -335,14 +366,17 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
     uint8_t* done = (uint8_t*)(redo + ((nblocks + 63) & ~63u));
     *redo_out = redo;
     ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
-              ptr, x_out_max, done, flags, best};
+              ptr, x_out_max, done, flags, best, nblocks * (x_out_max / kTile),
+              (uint32_t)__builtin_ctz(x_out_max / kTile)};
+    if ((x_out_max & (x_out_max - 1)) || x_out_max < kTile) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * 32, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(done, 0, (size_t)nblocks * (x_out_max / kXBytes), stream);
     if (e == hipSuccess) e = hipMemsetAsync(best, 0xFF, sizeof(uint32_t) * nblocks, stream);
     if (e == hipSuccess && f1) e = hipMemsetAsync(redo, 0, sizeof(uint32_t) * nblocks, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
     hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    const dim3 grid((x_out_max + kXThreads * kXBytes - 1) / (kXThreads * kXBytes), nblocks);
+    const dim3 grid(min(a.ntiles, kXGrid));
     hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
     hipLaunchKernelGGL(lz4mi_chase_kernel, grid, dim3(kXThreads), 0, stream, a);

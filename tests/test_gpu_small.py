@@ -39,6 +39,15 @@ def _blocks(rng):
     out.append(np.zeros(4 << 20, dtype=np.uint8))                                  # one offset-1 run
     out.append(np.resize(rng.integers(0, 256, 3, dtype=np.uint8), 3 << 20))       # period 3
     out.append(_far(rng, 2 << 20))
+    # long periodic runs (periods 1..300, one overlapping match each) between random runs: a low
+    # ratio, so the block takes the pointer path and its runs the period remap (ratio >= 32 blocks,
+    # like the two above, are decoded by one wave)
+    parts = []
+    for k in range(24):
+        parts.append(rng.integers(0, 256, 65536, dtype=np.uint8))
+        per = int(rng.integers(1, 301))
+        parts.append(np.resize(rng.integers(0, 256, per, dtype=np.uint8), 65536 + int(rng.integers(0, 999))))
+    out.append(np.concatenate(parts))
     out.append(O.generate("tiles216", 5, 100))
     out.append(np.zeros(0, dtype=np.uint8))
     out.append(O.generate("text", 9, 13))
