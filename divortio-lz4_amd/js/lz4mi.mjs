@@ -85,7 +85,7 @@ function blockId(bytes) {             // bufferCompress.js:77-82
 // PCIe copies, and the host b blocks one after another, so the GPU wins from a block count on
 // that is nearly independent of the block size. The crossovers below are measured on the box
 // (bench.py `single_block` and `napi_end_to_end.crossover`; 4 MiB tiles216: compress GPU
-// ~29 ms for one block vs host 1.1 ms per block -> 32 blocks). Decode of up to 48 blocks takes
+// ~29 ms for one block vs host 1.1 ms per block -> 32 blocks). Decode of up to 96 blocks takes
 // the small-batch path (64 waves per block, round 5): through N-API 0.41 ms per block + ~2.8 ms
 // against the host's ~1 ms per block (4 blocks 4.5 vs 3.8 ms, 16 blocks 9.4 vs 15.6), a
 // crossover at ~5 blocks; 8 keeps frames of a few blocks whose reference-mode decode needs the
