@@ -482,15 +482,6 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
     return make_uint4(ld_u32(j, p), ld_u32(j, p + 4), ld_u32(j, p + 8), ld_u32(j, p + 12));
 }
 
-#ifndef LZ4MI_LDS_TABLE
-#define LZ4MI_LDS_TABLE 0 // 1: the batch encoder's position table in LDS instead of global (A/B switch)
-#endif
-#ifndef LZ4MI_KMAX
-#define LZ4MI_KMAX 8      // probes per hit batch (<= kSpecK) (A/B switch)
-#endif
-#ifndef LZ4MI_KADAPT
-#define LZ4MI_KADAPT 0    // 1: next hit batch K = J + 2 after a batch ended at probe J < K - 1; 2: 2 (J + 1) (A/B switch)
-#endif
 #ifndef LZ4MI_DUPSLOT
 #define LZ4MI_DUPSLOT 1   // hit batches test for repeated hashes with an LDS slot before the DPP checks (A/B switch)
 #endif
@@ -519,12 +510,20 @@ struct GtsShared {
     uint8_t slot[1024];                  // miss batches: lane ids keyed by hash & 1023
     uint32_t code[kCodeWords];           // 2-bit epoch code per table entry
     uint32_t win[kWinBytes / 4 + 4];     // source bytes [wb, wb + kWinBytes)
-#if LZ4MI_LDS_TABLE
-    uint16_t tab[16384];                 // the 15-bit table in LDS (41 KB per block: 3 blocks per CU)
-#endif
 };
+// Small batches (<= kLdsTableMaxBlocks): the 15-bit table in LDS too (41 KB per block, 3 blocks
+// per CU, the batch one resident round): 1 block 26.7 -> 25.5 ms, 16: 32.4 -> 31.2, 256: 34.5
+// -> 32.9, 768: 42.4 -> 37.7 (profiles/r05f2/ldst_small.log); at 4096 blocks it needs 5.3 rounds
+// (200 vs 70 ms, profiles/r05n)
+struct GtsSharedL : GtsShared {
+    uint16_t tab[16384];
+};
+constexpr uint32_t kLdsTableMaxBlocks = 768;
+__device__ __forceinline__ uint16_t* gts_table(GtsShared&, int32_t* T) { return (uint16_t*)T; }
+__device__ __forceinline__ uint16_t* gts_table(GtsSharedL& F, int32_t*) { return F.tab; }
 
-__device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T, int lane) {
+template <class SH>
+__device__ int64_t compress_block_gts(const CompJob& j, SH& F, int32_t* T, int lane) {
     const int32_t n = j.len;
     const uint32_t n32 = (uint32_t)j.src_total;   // (= n: the block is the whole source)
     const int32_t mflimit = n - 12, matchlimit = n - 5;
@@ -532,22 +531,13 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
     int32_t i = 0, anchor = 0;
     uint32_t c = 67;
     int32_t S = 0;                       // step of the last hit (0: in a miss chain): the speculated probe distance
-#if LZ4MI_KADAPT
-    int kmax = LZ4MI_KMAX;               // probes of the next hit batch, sized from how far the last one got
-#else
-    const int kmax = LZ4MI_KMAX;
-#endif
+    const int kmax = kSpecK;
     // accepted sequences not emitted yet (lanes 0 .. npend-1: probe, candidate, match end),
     // emitted while the next batch's table reads are in flight
     int npend = 0;
     int32_t pd_p = 0, pd_c = 0, pd_e = 0;
     int32_t wb = -(1 << 30);             // F.win holds source [wb, wb + kWinBytes)
-#if LZ4MI_LDS_TABLE
-    uint16_t* T16 = F.tab;
-    (void)T;
-#else
-    uint16_t* T16 = (uint16_t*)T;
-#endif
+    uint16_t* T16 = gts_table(F, T);
     int32_t g = 0;
     for (int k = lane; k < 16384 / 8; k += kWave) ((uint4*)T16)[k] = make_uint4(0, 0, 0, 0);
     for (int k = lane; k < kCodeWords; k += kWave) F.code[k] = 0x55555555u;   // code 1: stale in epoch 0
@@ -759,11 +749,6 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
             insert(lane <= J && !later, h, p);
             const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);
             const bool hitJ = (__ballot(hit) >> J) & 1ull;
-#if LZ4MI_KADAPT == 1
-            kmax = J + 1 >= K ? LZ4MI_KMAX : min(LZ4MI_KMAX, J + 2);
-#elif LZ4MI_KADAPT == 2
-            kmax = J + 1 >= K ? LZ4MI_KMAX : min(LZ4MI_KMAX, 2 * (J + 1));
-#endif
             pd_p = p;
             pd_c = cand;
             pd_e = e;
@@ -841,9 +826,6 @@ __device__ int64_t compress_block_gts(const CompJob& j, GtsShared& F, int32_t* T
         const int mi = nprobe - 1;
         const int32_t pm = lane_val(pm_, mi), cm = lane_val(mc, mi);
         c = 67;
-#if LZ4MI_KADAPT
-        kmax = LZ4MI_KMAX;
-#endif
         const int32_t e1 = pm + 4 + (int32_t)match_extent(j, lane, pm + 4, cm + 4, matchlimit - (pm + 4));
         pd_p = pm;
         pd_c = cm;
@@ -870,8 +852,9 @@ __device__ unsigned long long g_ctl[2 * kCtlMax];   // per block: start, end (s_
 __device__ unsigned int g_ctl_id[2 * kCtlMax];      // per block: HW_ID, XCC_ID
 #endif
 
+template <class SH>
 __global__ __launch_bounds__(64, 4) void lz4mi_compress_gts_kernel(CompArgs a, int32_t* tables) {
-    __shared__ GtsShared F;
+    __shared__ SH F;
     const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
 #if LZ4MI_CTIMELINE
@@ -1208,7 +1191,12 @@ extern "C" hipError_t lz4mi_launch_compress(const uint8_t* in, const uint64_t* i
     a.in = in; a.in_off = in_off; a.in_len = in_len; a.out = out; a.out_off = out_off; a.out_len = out_len;
     a.nblocks = nblocks;
     // speculative hit-chain batch encoder, 16 blocks per CU; `tables` = per-block scratch
-    hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel, dim3(nblocks), dim3(64), 0, stream, a, tables);
+    if (nblocks <= lz4mi::kLdsTableMaxBlocks)   // one resident round at 3 blocks per CU: the table in LDS
+        hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel<lz4mi::GtsSharedL>, dim3(nblocks), dim3(64), 0, stream,
+                           a, tables);
+    else
+        hipLaunchKernelGGL(lz4mi::lz4mi_compress_gts_kernel<lz4mi::GtsShared>, dim3(nblocks), dim3(64), 0, stream,
+                           a, tables);
     return hipGetLastError();
 }
 
