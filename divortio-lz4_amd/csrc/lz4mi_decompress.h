@@ -29,10 +29,10 @@ struct DecArgs {
     uint4* xseq = nullptr;
     uint32_t* xcnt = nullptr;
     struct SegRec* xrec = nullptr;
-    uint32_t xseq_stride = 0;          // entries per segment
+    uint32_t xseq_stride = 0;          // entries per block (seg_geom: its segments at s * stride)
     uint32_t xsegs = 0;
     uint32_t x_in_max = 0, x_out_max = 0;
-    int xphase = 0;                    // 0: speculative parse; 1: re-parse from the first bad entry on
+    int xphase = 0;                    // 0: speculative parse; 2: re-parse of the disagreeing ones; 1: in order from the first bad entry
     const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
     uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)
     int xforce = 0;                    // test hook: every segment but the first counts as mis-guessed
@@ -49,11 +49,31 @@ struct SegRec {
     uint32_t olen;    // their output bytes
     uint32_t err;     // (index in the segment << 3) | check of its first parse error; 0xFFFFFFFF: none
     uint32_t fin;     // final exit + 1 once checked against the previous segment (0: not yet)
-    uint32_t base;    // output start of the segment (lz4mi_xcheck_kernel)
+    uint32_t base;    // output start of the segment (lz4mi_xbase_kernel; kNoBase: after the block's first error)
     uint32_t fail;    // the speculative parse met an error before the segment: its guess is wrong
+    uint32_t g0;      // number of the segment's first sequence in the block (lz4mi_xbase_kernel)
+    uint32_t from;    // phase 2: re-parse from this entry (kNoBase: no; lz4mi_xverify_kernel)
+    uint32_t pad[2];
 };
+constexpr uint32_t kNoBase = 0xFFFFFFFFu;
 constexpr uint32_t kFinErr = 0xFFFFFFFEu;
-constexpr uint32_t kSmallSegs = 64;          // segments (waves) per exported block   // fin - 1 of a segment at or after the block's first error
+constexpr uint32_t kSegMax = 256;            // segments (waves) per exported block, at most
+constexpr uint32_t kSegTarget = 8192;        // compressed bytes per segment (a 4 MiB tiles216 block: 64)
+// An exported block's segments: S of them, L compressed bytes each (the last takes the rest),
+// segment s's sequence entries at s * stride in the block's region (L / 3 sequences of >= 3
+// bytes, a failing one, the cut, and the 3 KiB warm-up's margin).
+struct SegGeom {
+    uint32_t S, L, stride;
+};
+__host__ __device__ inline SegGeom seg_geom(uint32_t in_len) {
+    uint32_t S = (in_len + kSegTarget - 1) / kSegTarget;
+    S = S < 1 ? 1 : (S > kSegMax ? kSegMax : S);
+    uint32_t L = ((in_len + S - 1) / S + 1023u) & ~1023u;
+    if (L < 4096) L = 4096;
+    return SegGeom{S, L, L / 3 + 1400};
+}
+// entries per block: every S * stride above (S * L <= in_len + S * 1024 + 4096) fits
+__host__ __device__ constexpr uint32_t seg_block_capacity(uint32_t x_in_max) { return x_in_max / 3 + kSegMax * 1800; }   // fin - 1 of a segment at or after the block's first error
 constexpr uint32_t kNotExported = 0xFFFFFFFFu;
 
 }  // namespace lz4mi

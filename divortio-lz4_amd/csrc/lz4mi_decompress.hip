@@ -1223,20 +1223,21 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const bool xp = XP && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max &&
                     (uint64_t)out_cap < (uint64_t)c.in_len * kXRatioMax;
     // past the export limits (or ratio >= 32): one wave decodes the block as usual -- segment
-    // b mod 64, i.e. workgroup 65 b (mod 256 CUs: a CU of its own for every block, where
-    // segment 0 would put the blocks of a batch on 4 CUs)
-    if (XP && !xp && sg != wblk % nseg) return;
+    // b mod 256, i.e. workgroup 257 b (mod 256 CUs: a CU of its own for every block, where
+    // segment 0 would put the blocks of a batch on one CU)
+    if (XP && !xp && (a.xphase != 0 || sg != wblk % nseg)) return;
     uint4* xs = nullptr;
     SegRec* xr = nullptr;
     uint32_t seg_lo = 0, seg_hi = 0;    // the segment: tokens in [seg_lo, seg_hi)
     if (XP && xp) {
-        const uint32_t L = max(4096u, (((uint32_t)c.in_len + nseg - 1) / nseg + 1023u) & ~1023u);
-        seg_lo = sg * L;
-        seg_hi = sg + 1 == nseg ? (uint32_t)c.in_len : min((uint32_t)c.in_len, seg_lo + L);
-        xs = a.xseq + ((size_t)wblk * nseg + sg) * a.xseq_stride;
+        const SegGeom G = seg_geom((uint32_t)c.in_len);   // S segments of ~kSegTarget bytes
+        if (sg >= G.S) return;
+        seg_lo = sg * G.L;
+        seg_hi = sg + 1 == G.S ? (uint32_t)c.in_len : min((uint32_t)c.in_len, seg_lo + G.L);
+        xs = a.xseq + (size_t)wblk * a.xseq_stride + (size_t)sg * G.stride;
         xr = a.xrec + (size_t)wblk * nseg + sg;
     }
-    if (XP && a.xphase == 1 && !xp) return;
+    if (XP && a.xphase != 0 && !xp) return;
     // export state (uniform): the entry found, done, the speculation failed, entry / exit tokens,
     // sequences exported, their output bytes, the first parse error; x_OG: output position of
     // the entry in this wave's running count; pass 1: the exact re-parse from x_entry
@@ -1244,6 +1245,17 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     uint32_t x_G = 0, x_X = 0, nx = 0, x_olen = 0, x_err = 0xFFFFFFFFu, x_entry = 0;
     int64_t x_OG = 0;
     int x_pass = 0;
+    if (XP && xp && a.xphase == 2) {
+        // phase 2: every segment whose guess disagrees with the previous one's exit, re-parsed
+        // from that exit at once (lz4mi_xverify_kernel's `from`), a guess again -- the check then
+        // runs again: a wrong guess does not make the later guesses wrong, and the segments
+        // before a wrong one are mostly right (text, ~10 % of ~190 segments: chained one after
+        // another in phase 1, 2.1 ms for a block)
+        const uint32_t from = uniform(xr->from);
+        if (from == kNoBase) return;
+        x_pass = 2;
+        x_entry = from;
+    }
     if (XP && xp && a.xphase == 1) {
         // phase 1: segments from the first wrong entry on, in order: re-parse from the previous
         // segment's final exit unless the speculative entry equals it
@@ -1872,7 +1884,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             xr->cnt = nx;
             xr->olen = x_olen;
             xr->err = x_err;
-            xr->fail = (x_fail || (a.xforce && sg > 0)) ? 1u : 0u;
+            xr->fail = (x_fail || (a.xforce && sg > 0 && x_pass == 0)) ? 1u : 0u;   // (re-parses: exact)
             if (x_pass == 1)   // the exact re-parse of phase 1: final
                 __hip_atomic_store(&xr->fin, (x_err != 0xFFFFFFFFu ? kFinErr : x_X) + 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1918,50 +1930,119 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_x_kernel(DecArgs a) { 
 // previous one's exit is final (fin), and one the chain passes over is empty; xfirst[b] = the
 // first segment that is neither (xsegs: none), re-parsed by phase 1.
 __global__ __launch_bounds__(64) void lz4mi_xverify_kernel(DecArgs a) {
-    static_assert(kSmallSegs == 64, "one lane per segment");
+    static_assert(kSegMax == 4 * 64, "four records per lane");
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (a.xcnt[b] == kNotExported) return;
     const uint32_t nseg = a.xsegs, in_len = a.in_len[b];
-    const uint32_t L = max(4096u, ((in_len + nseg - 1) / nseg + 1023u) & ~1023u);
+    const SegGeom G = seg_geom(in_len);
     SegRec* R = a.xrec + (size_t)b * nseg;
-    // the records, one per lane, in one round trip; then the walk in registers
-    const uint32_t entry = R[lane].entry, exit = R[lane].exit, err = R[lane].err, fail = R[lane].fail;
-    const uint32_t hi_l = lane + 1 == nseg ? in_len : min(in_len, lane * L + L);
-    uint32_t first = nseg, prev = 0;   // prev: the previous segment's final exit (kFinErr: an error)
-    uint32_t my_fin = 0, kind = 0;     // kind: 0 as parsed, 1 empty (after an error / passed over)
-    for (uint32_t sg = 0; sg < nseg; ++sg) {
-        const uint32_t hi = __builtin_amdgcn_readlane(hi_l, sg);
-        const uint32_t en = __builtin_amdgcn_readlane(entry, sg), ex = __builtin_amdgcn_readlane(exit, sg);
-        const uint32_t er = __builtin_amdgcn_readlane(err, sg), fl = __builtin_amdgcn_readlane(fail, sg);
-        uint32_t fin, k = 0;
-        if (sg > 0 && prev == kFinErr) {
-            fin = kFinErr;
-            k = 1;
-        } else if (sg > 0 && prev >= hi) {
-            fin = prev;
-            k = 1;
-        } else if (sg == 0 || (!fl && en == prev)) {
-            fin = er != 0xFFFFFFFFu ? kFinErr : ex;
-        } else {
-            first = sg;
-            break;
-        }
-        if (lane == sg) {
-            my_fin = fin;
-            kind = k;
-        }
-        prev = fin;
+    // the records, four per lane (segment 64 q + lane), in one round trip; then the walk in registers
+    uint32_t entry[4], exit[4], err[4], fail[4], hi_l[4], my_fin[4], kind[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        const bool in = sg < G.S;
+        entry[q] = in ? R[sg].entry : 0u;
+        exit[q] = in ? R[sg].exit : 0u;
+        err[q] = in ? R[sg].err : 0xFFFFFFFFu;
+        fail[q] = in ? R[sg].fail : 0u;
+        hi_l[q] = sg + 1 >= G.S ? in_len : min(in_len, sg * G.L + G.L);
+        my_fin[q] = 0;
+        kind[q] = 0;                   // 0 as parsed, 1 empty (after an error / passed over)
     }
-    if (lane < first) {
-        if (kind) {   // nothing here: after the block's first error, or the chain passes over it
-            if (my_fin != kFinErr) R[lane].entry = R[lane].exit = my_fin;
-            R[lane].cnt = 0;
-            R[lane].olen = 0;
-            R[lane].err = 0xFFFFFFFFu;
+    // the previous segment's exit and error, per lane
+    uint32_t pex[4], per[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        pex[q] = __shfl_up(exit[q], 1);
+        per[q] = __shfl_up(err[q], 1);
+        if (lane == 0) {
+            pex[q] = q ? __builtin_amdgcn_readlane(exit[q > 0 ? q - 1 : 0], 63) : 0u;
+            per[q] = q ? __builtin_amdgcn_readlane(err[q > 0 ? q - 1 : 0], 63) : 0xFFFFFFFFu;
         }
-        R[lane].fin = my_fin + 1u;
+    }
+    // the usual case at once: segment 0, and every one after it whose guess the previous one's
+    // exit confirms (no error before it, no segment passed over) -- final up to s0, the first
+    // that is not (the walk below, one segment at a time, goes on from there)
+    uint32_t s0 = G.S;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+        const uint32_t sg = 64u * q + lane;
+        const bool ok = sg < G.S && (sg == 0 || (!fail[q] && entry[q] == pex[q] && per[q] == 0xFFFFFFFFu &&
+                                                 pex[q] < hi_l[q]));
+        const uint64_t bad = __ballot(sg < G.S && !ok);
+        if (bad) s0 = 64u * q + (uint32_t)__builtin_ctzll(bad);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (64u * q + lane < s0) my_fin[q] = err[q] != 0xFFFFFFFFu ? kFinErr : exit[q];
+    uint32_t first = G.S, prev = 0;    // prev: the previous segment's final exit (kFinErr: an error)
+    if (s0 > 0 && s0 < G.S) {
+        const uint32_t t = s0 - 1;
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if ((t >> 6) == (uint32_t)q) v = __builtin_amdgcn_readlane(my_fin[q], t & 63);
+        prev = v;
+    }
+    bool stop = s0 >= G.S;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (stop || 64u * q + 63 < s0) continue;
+        for (uint32_t l = 64u * q < s0 ? s0 - 64u * q : 0u; l < 64 && !stop; ++l) {
+            const uint32_t sg = 64u * q + l;
+            if (sg >= G.S) {
+                stop = true;
+                break;
+            }
+            const uint32_t hi = __builtin_amdgcn_readlane(hi_l[q], l);
+            const uint32_t en = __builtin_amdgcn_readlane(entry[q], l), ex = __builtin_amdgcn_readlane(exit[q], l);
+            const uint32_t er = __builtin_amdgcn_readlane(err[q], l), fl = __builtin_amdgcn_readlane(fail[q], l);
+            uint32_t fin, k = 0;
+            if (sg > 0 && prev == kFinErr) {
+                fin = kFinErr;
+                k = 1;
+            } else if (sg > 0 && prev >= hi) {
+                fin = prev;
+                k = 1;
+            } else if (sg == 0 || (!fl && en == prev)) {
+                fin = er != 0xFFFFFFFFu ? kFinErr : ex;
+            } else {
+                first = sg;
+                stop = true;
+                break;
+            }
+            if (lane == l) {
+                my_fin[q] = fin;
+                kind[q] = k;
+            }
+            prev = fin;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        if (sg < first) {
+            if (kind[q]) {   // nothing here: after the block's first error, or the chain passes over it
+                if (my_fin[q] != kFinErr) R[sg].entry = R[sg].exit = my_fin[q];
+                R[sg].cnt = 0;
+                R[sg].olen = 0;
+                R[sg].err = 0xFFFFFFFFu;
+            }
+            R[sg].fin = my_fin[q] + 1u;
+        }
     }
     if (lane == 0) a.xfirst_w[b] = first;
+    // the re-parse of phase 2: from the previous segment's exit where a segment at or past the
+    // first unchecked one disagrees with it (and that one met no error, its guess did not fail,
+    // and it does not pass over this one)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        const bool redo = sg < G.S && sg >= first && sg > 0 && (fail[q] || entry[q] != pex[q]) &&
+                          per[q] == 0xFFFFFFFFu && pex[q] >= sg * G.L && pex[q] < hi_l[q];   // (a failed guess: exit 0)
+        if (sg < G.S) R[sg].from = redo ? pex[q] : kNoBase;
+    }
 }
 
 // Dispatch order of a batch (LZ4MI_ORDER). Every block is one wave and a batch of up to
@@ -2057,28 +2138,25 @@ extern "C" hipError_t lz4mi_launch_decompress(const uint8_t* in, const uint64_t*
     return hipGetLastError();
 }
 
-extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, uint8_t*, const uint64_t*, const uint32_t*,
+extern "C" hipError_t lz4mi_launch_expand(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*, const uint64_t*,
+                                          const uint32_t*,
                                           const uint8_t*, uint32_t, uint32_t*, int32_t*, const uint4*, const uint32_t*,
                                           lz4mi::SegRec*, uint32_t, uint32_t, uint32_t*, uint32_t, uint32_t*, int,
                                           uint32_t**, uint32_t, hipStream_t);
 
-// A small batch in LZ4 spec mode (lz4mi_expand.hip): each block within the export limits
-// (x_in_max compressed, x_out_max output bytes) is parsed by kSmallSegs waves, one per segment
-// of its compressed bytes, which export its sequences instead of writing them; the whole GPU
-// then computes the output by pointer jumping. A block past the limits is decoded by the same
-// launch as usual. `xs` scratch (lz4mi_small_scratch_bytes): the segments' sequence entries,
-// the blocks' counts and segment records, nblocks * x_out_max pointers, the jump rounds' flags.
-using lz4mi::kSmallSegs;
-__host__ __device__ constexpr uint32_t small_seg_stride(uint32_t x_in_max) {
-    // a segment is at most max(4096, ceil(x_in_max / kSmallSegs) rounded up to 1 KiB) bytes;
-    // its sequences (>= 3 bytes each but the last), a failing one and the cut: L / 3 + 16
-    return (((x_in_max + kSmallSegs - 1) / kSmallSegs + 1023u) & ~1023u) / 3u + 4096u / 3u + 16u;
-}
+// A small batch in LZ4 spec or reference mode (lz4mi_expand.hip): each block within the export
+// limits (x_in_max compressed, x_out_max output bytes, ratio < 32) is parsed by up to kSegMax
+// waves, one per ~kSegTarget bytes of its compressed block (seg_geom), which export its
+// sequences instead of writing them; the whole GPU then computes the output by pointer jumping.
+// Other blocks are decoded by the same launch as usual. `xs` scratch (lz4mi_small_scratch_bytes):
+// the blocks' sequence entries, their counts, first wrong segments and segment records,
+// nblocks * x_out_max pointers, and the output kernels' flags.
+using lz4mi::kSegMax;
 static size_t small_meta_bytes(uint32_t nblocks) {   // counts, first wrong segments, segment records
-    return ((size_t)nblocks * 8 + (size_t)nblocks * lz4mi::kSmallSegs * sizeof(lz4mi::SegRec) + 255) / 256 * 256;
+    return ((size_t)nblocks * 8 + (size_t)nblocks * kSegMax * sizeof(lz4mi::SegRec) + 255) / 256 * 256;
 }
 extern "C" size_t lz4mi_small_scratch_bytes(uint32_t nblocks, uint32_t x_in_max, uint32_t x_out_max) {
-    const size_t seqs = (size_t)nblocks * kSmallSegs * small_seg_stride(x_in_max) * 16;
+    const size_t seqs = (size_t)nblocks * lz4mi::seg_block_capacity(x_in_max) * 16;
     return (seqs + 255) / 256 * 256 + small_meta_bytes(nblocks) + (size_t)nblocks * x_out_max * 4 +
            128 + ((size_t)nblocks + 63) / 64 * 512 + (size_t)nblocks * (x_out_max / 16) + 256;
 }
@@ -2090,10 +2168,10 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
                                                     hipStream_t stream) {
     using lz4mi::SegRec;
     if (nblocks == 0) return hipSuccess;
-    const uint32_t stride = small_seg_stride(x_in_max);
+    const uint32_t stride = lz4mi::seg_block_capacity(x_in_max);
     uint8_t* p = (uint8_t*)xs;
     uint4* xseq = (uint4*)p;
-    p += ((size_t)nblocks * kSmallSegs * stride * 16 + 255) / 256 * 256;
+    p += ((size_t)nblocks * stride * 16 + 255) / 256 * 256;
     uint32_t* xcnt = (uint32_t*)p;
     uint32_t* xfirst = xcnt + nblocks;
     SegRec* xrec = (SegRec*)(xfirst + nblocks);
@@ -2110,25 +2188,32 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     a.xcnt = xcnt;
     a.xrec = xrec;
     a.xseq_stride = stride;
-    a.xsegs = kSmallSegs;
+    a.xsegs = kSegMax;
     a.x_in_max = x_in_max;
     a.x_out_max = x_out_max;
     a.xfirst = xfirst;
     a.xfirst_w = xfirst;
     a.xforce = force_reparse;
     // phase 0: every segment speculatively; the check; phase 1: the segments from the first
-    // wrong entry on (an empty launch when there is none). Every wave of a launch is resident at
-    // once (<= 16 blocks x 64 segments), so a phase-1 wave's wait for its predecessor ends.
-    const dim3 grid(nblocks * kSmallSegs);
+    // wrong entry on (an empty launch when there is none). A phase-1 wave waits only for its
+    // predecessor, whose workgroup index is lower (dispatched first): the wait always ends.
+    const dim3 grid(nblocks * kSegMax);
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    // phase 2 (twice): the segments whose guesses disagree, re-parsed at once, then the check
+    // again; phase 1 chains what is left
+    a.xphase = 2;
+    for (int k = 0; k < 2; ++k) {
+        hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
+        hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
+    }
     a.xphase = 1;
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     uint32_t* redo = nullptr;
-    e = lz4mi_launch_expand(in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
-                            kSmallSegs, stride, ptr, x_out_max, aux, f1, &redo, nblocks, stream);
+    e = lz4mi_launch_expand(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
+                            kSegMax, stride, ptr, x_out_max, aux, f1, &redo, nblocks, stream);
     if (e != hipSuccess || !f1) return e;
     // reference mode (LZ4MI_JS_EXACT): the blocks whose output a double-copy-tail rewrite would
     // change (lz4mi_xf1_kernel) are decoded again by the batch kernel's in-chunk fix-up; the

@@ -40,6 +40,7 @@ constexpr int kJumpRounds = 10;          // doubling rounds; then lz4mi_chase_ke
 struct ExpArgs {
     const uint8_t* in;
     const uint64_t* in_off;
+    const uint32_t* in_len;
     uint8_t* out;
     const uint64_t* out_off;
     const uint32_t* out_cap;
@@ -51,7 +52,7 @@ struct ExpArgs {
     const uint32_t* xcnt;
     SegRec* xrec;
     uint32_t nseg;
-    uint32_t xseq_stride;
+    uint32_t xseq_stride;     // sequence entries per block (segment s at s * seg_geom(in_len).stride)
     uint32_t* ptr;            // x_out_max pointers per block
     uint32_t x_out_max;
     uint8_t* done;            // per block and 16 output bytes (one thread's): its pointers are all resolved
@@ -80,34 +81,94 @@ __device__ __forceinline__ uint8_t* done_flag(const ExpArgs& a, uint32_t b, uint
     return a.done + (size_t)b * (a.x_out_max / kXBytes) + t * kXThreads + threadIdx.x;
 }
 
-// The segments before sg (all final): sg's output start and first sequence number, and
-// whether the block stopped at an error before sg (the parse's error, as its sequence code)
-__device__ __forceinline__ bool seg_prefix(const SegRec* R, uint32_t sg, uint32_t& base, uint32_t& g0, uint32_t& perr) {
-    base = g0 = 0;
-    perr = 0xFFFFFFFFu;
-    for (uint32_t s = 0; s < sg; ++s) {
-        if (R[s].fin == kFinErr + 1u) return false;
-        base += R[s].olen;
-        g0 += R[s].cnt;
-    }
-    if (R[sg].fin == kFinErr + 1u && R[sg].err != 0xFFFFFFFFu) perr = ((g0 + (R[sg].err >> 3)) << 3) | (R[sg].err & 7u);
-    return true;
+__device__ __forceinline__ const uint4* seg_entries(const ExpArgs& a, uint32_t b, uint32_t sg, const SegGeom& G) {
+    return a.xseq + (size_t)b * a.xseq_stride + (size_t)sg * G.stride;
 }
 
-// Per (segment, block) after the parse: the segment's output start, and the reference's checks
-// that need absolute output positions (1 capacity, 4 dictionary bounds, 5 cross-block; the parse
-// did 2 and 3) on its sequences: min of (sequence << 3 | check) over the failing ones, which is
-// the first check the reference's decoder fails (blockDecompress.js), into best[b].
+// Per block after the parse (one wave, four segment records per lane): every segment's output
+// start and first sequence number (exclusive scans in segment order), the first segment at an
+// error (stop) -- the ones after it get kNoBase --, the parse's first error as
+// (sequence << 3 | check) into best[b], the output length into out_len[b].
+__global__ __launch_bounds__(64) void lz4mi_xbase_kernel(ExpArgs a) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.xcnt[b] == kNotExported) return;
+    const SegGeom G = seg_geom(a.in_len[b]);
+    SegRec* R = a.xrec + (size_t)b * a.nseg;
+    uint32_t olen[4], cnt[4], fe[4];
+    uint64_t em = 0;
+    uint32_t stop = G.S;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        const bool in = sg < G.S;
+        const bool e = in && R[sg].fin == kFinErr + 1u;
+        olen[q] = in ? R[sg].olen : 0u;
+        cnt[q] = in ? R[sg].cnt : 0u;
+        fe[q] = e ? 1u : 0u;
+        const uint64_t m = __ballot(e);
+        if (m && stop == G.S) stop = 64u * q + (uint32_t)__builtin_ctzll(m);
+        em |= m;
+    }
+    uint32_t base = 0, g = 0;   // running totals of the quarters before
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        uint32_t io = olen[q], ic = cnt[q];   // inclusive scans over the quarter's lanes
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t po = __shfl_up(io, d), pc = __shfl_up(ic, d);
+            if (lane >= (uint32_t)d) {
+                io += po;
+                ic += pc;
+            }
+        }
+        if (sg < G.S) {
+            R[sg].base = sg <= stop ? base + io - olen[q] : kNoBase;
+            R[sg].g0 = g + ic - cnt[q];
+        }
+        base += __shfl(io, 63);
+        g += __shfl(ic, 63);
+    }
+    // totals of the segments before `stop`, the parse error at `stop`
+    uint32_t tb = 0, tg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sg = 64u * q + lane;
+        const bool before = sg < stop;
+        uint32_t vo = before ? olen[q] : 0u, vc = before ? cnt[q] : 0u;
+        for (int d = 32; d >= 1; d >>= 1) {
+            vo += __shfl_xor(vo, d);
+            vc += __shfl_xor(vc, d);
+        }
+        tb += vo;
+        tg += vc;
+    }
+    if (lane == 0) {
+        uint32_t perr = 0xFFFFFFFFu;
+        if (stop < G.S) {
+            const uint32_t er = R[stop].err;
+            if (er != 0xFFFFFFFFu) perr = ((tg + (er >> 3)) << 3) | (er & 7u);
+        }
+        a.best[b] = perr;
+        a.out_len[b] = tb;
+    }
+    (void)fe;
+}
+
+// Per (segment, block): the reference's checks that need absolute output positions (1 capacity,
+// 4 dictionary bounds, 5 cross-block; the parse did 2 and 3) on the segment's sequences: the
+// minimum of (sequence << 3 | check) over the failing ones, with the parse's error, is the
+// first check the reference's decoder fails (blockDecompress.js) -> best[b].
 __global__ __launch_bounds__(kXThreads) void lz4mi_xcheck_kernel(ExpArgs a, int isolate) {
     const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (a.xcnt[b] == kNotExported) return;
-    SegRec* R = a.xrec + (size_t)b * a.nseg;
-    uint32_t base, g0, perr;
-    if (!seg_prefix(R, sg, base, g0, perr)) return;   // after the block's first error
-    if (threadIdx.x == 0) R[sg].base = base;
+    const SegGeom G = seg_geom(a.in_len[b]);
+    if (sg >= G.S) return;
+    const SegRec* R = a.xrec + (size_t)b * a.nseg;
+    const uint32_t base = R[sg].base, g0 = R[sg].g0;
+    if (base == kNoBase) return;                       // after the block's first error
     const int64_t cap = a.out_cap[b] > 0x7FFFFFFFu ? 0x7FFFFFFF : (int64_t)a.out_cap[b];
     const int64_t out_off = (int64_t)a.out_off[b], dict_len = a.dict ? (int64_t)a.dict_len : 0;
-    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+    const uint4* E = seg_entries(a, b, sg, G);
     const uint32_t cnt = R[sg].cnt;
     uint32_t mine = 0xFFFFFFFFu;
     for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
@@ -122,31 +183,17 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_xcheck_kernel(ExpArgs a, int 
     if (mine != 0xFFFFFFFFu) atomicMin(&a.best[b], mine);
 }
 
-// Per block: status and output length from the parse's first error and the checks above
-// (one lane per segment record, loaded in one round trip).
+// Per block: status and output length from the first failing check (best[b]).
 __global__ __launch_bounds__(64) void lz4mi_xstatus_kernel(ExpArgs a) {
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
-    if (a.xcnt[b] == kNotExported) return;
-    const SegRec* R = a.xrec + (size_t)b * a.nseg;
-    const bool in = lane < a.nseg;
-    const uint32_t fin = in ? R[lane].fin : 0u, olen = in ? R[lane].olen : 0u, cnt = in ? R[lane].cnt : 0u;
-    const uint32_t err = in ? R[lane].err : 0xFFFFFFFFu;
-    const uint64_t em = __ballot(in && fin == kFinErr + 1u);
-    const uint32_t stop = em ? (uint32_t)__builtin_ctzll(em) : a.nseg;   // the first segment at an error
-    // prefix sums of the segments before `stop`
-    uint32_t base = 0, g0 = 0;
-    for (uint32_t s = 0; s < stop; ++s) {
-        base += __builtin_amdgcn_readlane(olen, s);
-        g0 += __builtin_amdgcn_readlane(cnt, s);
+    const uint32_t b = blockIdx.x;
+    if (threadIdx.x != 0 || a.xcnt[b] == kNotExported) return;
+    const uint32_t e = a.best[b];
+    if (e != 0xFFFFFFFFu) {
+        a.status[b] = (e & 7u) == 5 ? -9 : -(int32_t)(e & 7u);
+        a.out_len[b] = 0;
+    } else {
+        a.status[b] = 0;
     }
-    if (lane != 0) return;
-    uint32_t e = a.best[b];
-    if (em) {
-        const uint32_t er = __builtin_amdgcn_readlane(err, stop);
-        if (er != 0xFFFFFFFFu) e = min(e, ((g0 + (er >> 3)) << 3) | (er & 7u));
-    }
-    a.status[b] = e == 0xFFFFFFFFu ? 0 : ((e & 7u) == 5 ? -9 : -(int32_t)(e & 7u));
-    a.out_len[b] = e == 0xFFFFFFFFu ? base : 0u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
@@ -157,11 +204,18 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
     const uint32_t n = x_span(a, b, X_T(a), x0);
     if (n) {
         const SegRec* R = a.xrec + (size_t)b * a.nseg;
-        // the segment holding x0, then its last sequence starting at or before x0
-        uint32_t sg = 0;
-        while (x0 >= R[sg].base + R[sg].olen) ++sg;
+        const SegGeom G = seg_geom(a.in_len[b]);
+        // the segment holding x0 (the first whose end is past it), then its last sequence
+        // starting at or before x0
+        uint32_t slo = 0, shi = G.S - 1;
+        while (slo < shi) {
+            const uint32_t mid = (slo + shi) >> 1;
+            if (R[mid].base + R[mid].olen > x0) shi = mid;
+            else slo = mid + 1;
+        }
+        uint32_t sg = slo;
         uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
-        const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+        const uint4* E = seg_entries(a, b, sg, G);
         uint32_t lo = 0, hi = cnt;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -187,7 +241,7 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
                         send = base + R[sg].olen;
                         cnt = R[sg].cnt;
                     } while (send == base);
-                    E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+                    E = seg_entries(a, b, sg, G);
                     k = 0;
                 }
                 e = E[k];
@@ -289,9 +343,11 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
 __global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int isolate, uint32_t* redo) {
     const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return;
+    const SegGeom G = seg_geom(a.in_len[b]);
+    if (sg >= G.S) return;
     const SegRec* R = a.xrec + (size_t)b * a.nseg;
     const uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
-    const uint4* E = a.xseq + ((size_t)b * a.nseg + sg) * a.xseq_stride;
+    const uint4* E = seg_entries(a, b, sg, G);
     const int64_t out_off = (int64_t)a.out_off[b];
     const int64_t cap = min(a.out_len[b], a.out_cap[b]);
     const uint8_t* dst = a.out + out_off;
@@ -352,7 +408,7 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
 // expand, up to kJumpRounds jump rounds (each returns at once when the previous one left
 // nothing to follow; a thread whose 16 bytes are resolved at once too), gather. `aux`: the round
 // flags (32 words), nblocks check results, then nblocks * x_out_max / 16 done bytes.
-extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, uint8_t* out,
+extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                           const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict,
                                           uint32_t dict_len, uint32_t* out_len, int32_t* status, const uint4* xseq,
                                           const uint32_t* xcnt, lz4mi::SegRec* xrec, uint32_t nseg,
@@ -365,15 +421,15 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
     uint32_t* redo = best + ((nblocks + 63) & ~63u);
     uint8_t* done = (uint8_t*)(redo + ((nblocks + 63) & ~63u));
     *redo_out = redo;
-    ExpArgs a{in, in_off, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
+    ExpArgs a{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec, nseg, xseq_stride,
               ptr, x_out_max, done, flags, best, nblocks * (x_out_max / kTile),
               (uint32_t)__builtin_ctz(x_out_max / kTile)};
     if ((x_out_max & (x_out_max - 1)) || x_out_max < kTile) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * 32, stream);
     if (e == hipSuccess) e = hipMemsetAsync(done, 0, (size_t)nblocks * (x_out_max / kXBytes), stream);
-    if (e == hipSuccess) e = hipMemsetAsync(best, 0xFF, sizeof(uint32_t) * nblocks, stream);
     if (e == hipSuccess && f1) e = hipMemsetAsync(redo, 0, sizeof(uint32_t) * nblocks, stream);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lz4mi_xbase_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(lz4mi_xcheck_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0);
     hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     const dim3 grid(min(a.ntiles, kXGrid));
