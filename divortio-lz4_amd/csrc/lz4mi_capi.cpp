@@ -179,7 +179,7 @@ hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32
         small->ensure(lz4mi_small_scratch_bytes(nblocks, kSmallInMax, kSmallOutMax), s) == hipSuccess)
         return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
                                              status, nblocks, kSmallInMax, kSmallOutMax, small->p,
-                                             std::getenv("LZ4MI_SMALL_REPARSE") ? 1 : 0,   // (test hook)
+                                             std::getenv("LZ4MI_SMALL_REPARSE") ? std::atoi(std::getenv("LZ4MI_SMALL_REPARSE")) : 0,   // (test hook)
                                              mode == 2 ? 1 : 0, s);
     uint32_t* ord = nullptr;
     if (order && nblocks > 1 && order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();

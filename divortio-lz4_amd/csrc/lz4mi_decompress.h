@@ -35,7 +35,7 @@ struct DecArgs {
     int xphase = 0;                    // 0: speculative parse; 2: re-parse of the disagreeing ones; 1: in order from the first bad entry
     const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
     uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)
-    int xforce = 0;                    // test hook: every segment but the first counts as mis-guessed
+    int xforce = 0;                    // test hook: every guess of segments past the first counts as wrong (1: phase 0's, 2: phase 2's too)
     const uint32_t* redo = nullptr;    // batch kernel: decode only the blocks with redo[b] != 0 (nullptr: all)
 };
 // One segment of an exported block. Its wave parses from a guessed entry (the first token at or

@@ -1884,7 +1884,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
             xr->cnt = nx;
             xr->olen = x_olen;
             xr->err = x_err;
-            xr->fail = (x_fail || (a.xforce && sg > 0 && x_pass == 0)) ? 1u : 0u;   // (re-parses: exact)
+            xr->fail = (x_fail || (a.xforce && sg > 0 && (a.xforce == 2 ? x_pass != 1 : x_pass == 0))) ? 1u : 0u;
             if (x_pass == 1)   // the exact re-parse of phase 1: final
                 __hip_atomic_store(&xr->fin, (x_err != 0xFFFFFFFFu ? kFinErr : x_X) + 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);

@@ -172,14 +172,15 @@ def _straddle_block(rng, n):
     return np.concatenate(parts)[:n]
 
 
-@pytest.mark.parametrize("force", [False, True])
+@pytest.mark.parametrize("force", [0, 1, 2])
 def test_small_batch_segment_reparse(force, monkeypatch):
-    """Segments whose speculative entry is wrong are re-parsed from the previous segment's exit
-    (phase 1): natural mis-guesses (literal runs across segment starts) and, with the test hook
-    LZ4MI_SMALL_REPARSE, every segment past the first re-parsed in order; errors inside a
-    re-parsed segment keep the reference's first-error order."""
+    """Segments whose speculative entry is wrong are re-parsed from the previous segment's exit:
+    natural mis-guesses (literal runs across segment starts, text) and, with the test hook
+    LZ4MI_SMALL_REPARSE, every first guess past segment 0 wrong (1: phase 2 re-parses them all at
+    once) or every guess (2: phase 1 re-parses them in order); errors inside a re-parsed segment
+    keep the reference's first-error order."""
     if force:
-        monkeypatch.setenv("LZ4MI_SMALL_REPARSE", "1")
+        monkeypatch.setenv("LZ4MI_SMALL_REPARSE", str(force))
     rng = np.random.default_rng(2718)
     srcs = [_straddle_block(rng, int(n)) for n in (4 << 20, 3 << 20, 1 << 20, 777777)]
     srcs += [O.generate(k, 31, 2 << 20) for k in ("text", "copy", "repetitive", "random")]
