@@ -137,6 +137,7 @@ constexpr int kLaneBytes = 256;               // longer runs are written by the 
 constexpr int kPeriodBulk = 1024;             // longer periodic runs are generated from an LDS copy of the pattern
 constexpr int32_t kLongLit = 4096;
 constexpr uint64_t kXRatioMax = 32;           // XP: blocks of higher ratio are decoded by one wave
+constexpr int kSegRestarts = 16;              // XP: a guess's walk starts over at most this often
 constexpr uint32_t kSegWarm = 3072;           // XP: a segment's warm-up parse (tiles216: 99 % of wrong
                                               // starts join the token chain within 860 bytes)            // literal runs at least this long: long_literals()
 
@@ -1244,7 +1245,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     bool x_started = false, x_done = false, x_fail = false;
     uint32_t x_G = 0, x_X = 0, nx = 0, x_olen = 0, x_err = 0xFFFFFFFFu, x_entry = 0;
     int64_t x_OG = 0;
-    int x_pass = 0;
+    int x_pass = 0, x_restart = 0;
     if (XP && xp && a.xphase == 2) {
         // phase 2: every segment whose guess disagrees with the previous one's exit, re-parsed
         // from that exit at once (lz4mi_xverify_kernel's `from`), a guess again -- the check then
@@ -1617,9 +1618,18 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 if (k0 == ntot && m0) k0 = 64u * r + (uint32_t)__builtin_ctzll(m0);
                 if (k1 == ntot && m1) k1 = 64u * r + (uint32_t)__builtin_ctzll(m1);
             }
+            bool restart = false;
             if (!x_started && fk < k0) {
-                // an error before the segment: a wrong guess, or an earlier segment's error
-                x_fail = x_done = true;
+                // an error before the segment: a wrong walk, or an earlier segment's error (which
+                // that segment's parse reports) -- never this segment's. A guess starts over one
+                // byte past the impossible token (text: an offset of 0 read from the wrong bytes
+                // failed 22 of a 4 MiB block's 255 guesses, which then waited for re-parses)
+                if (x_pass == 0 && x_restart < kSegRestarts) {
+                    restart = true;
+                    ++x_restart;
+                } else {
+                    x_fail = x_done = true;
+                }
             } else {
                 if (!x_started && k0 < ntot) {
                     x_started = true;
@@ -1650,7 +1660,10 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     nx += ke - k0;
                 }
             }
-            if (!x_done) {   // on to the next chunk
+            if (restart) {
+                c.ip = (int32_t)(x_tok(fk) + 1u);
+                c.O = 0;
+            } else if (!x_done) {   // on to the next chunk
                 if (cut) {
                     c.O = tab_hi + cll + cml;
                     c.ip = (int32_t)(cq < c.in_len ? cq : c.in_len);
@@ -2200,13 +2213,12 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     const dim3 grid(nblocks * kSegMax);
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    // phase 2 (twice): the segments whose guesses disagree, re-parsed at once, then the check
-    // again; phase 1 chains what is left
+    // phase 2: the segments whose guesses disagree, re-parsed at once, then the check again;
+    // phase 1 chains what is left (a second phase-2 pass: ~11 us of empty launches per call
+    // once the guesses restart past impossible tokens)
     a.xphase = 2;
-    for (int k = 0; k < 2; ++k) {
-        hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
-        hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
-    }
+    hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(lz4mi::lz4mi_xverify_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     a.xphase = 1;
     hipLaunchKernelGGL(lz4mi::lz4mi_decompress_x_kernel, grid, dim3(64), 0, stream, a);
     e = hipGetLastError();

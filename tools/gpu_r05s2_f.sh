@@ -1,6 +1,6 @@
 # small-batch decode, adaptive segments (<= 256 of ~8 KiB) with phase 2 (the first wrong segment
 # (all of them at once, twice), then the check again): the GPU suite, latency, per-dispatch kernel times
-cd $GRAFT_REPO_ROOT && T=${1:-r05s2_h} && mkdir -p gpurun_out/$T
+cd $GRAFT_REPO_ROOT && T=${1:-r05s2_k} && mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_small.py -m gpu -x -v --timeout 120 --timeout-method thread 2>&1 | grep -v amdgpu.ids | tee gpurun_out/$T/small.log || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread 2>&1 | grep -v amdgpu.ids | tee gpurun_out/$T/tests.log || exit 1
