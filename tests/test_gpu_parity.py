@@ -193,23 +193,27 @@ def test_fuzz_roundtrip_and_corruption():
                 c[rng.integers(0, c.size)] = rng.integers(0, 256)
         bad.append(c)
         caps.append(srcs[t].size + (t % 3) * 7)
-    for js in (False, True):
+    # spec mode as 48 blocks (the small-batch path) and as the same blocks three times (144: the
+    # batch kernel); reference-compatible mode one block at a time
+    for js, rep in ((False, 1), (False, 3), (True, 1)):
         if js:     # one output array per block (see test_decompress_reference_blocks_spec_and_jscompat)
             res = [lz4mi.decompress_blocks([c], [k], js_compat=True) for c, k in zip(bad, caps)]
             st = [r[0][0] for r in res]
             outs = [r[1][0] for r in res]
             lens = [r[2][0] for r in res]
         else:
-            st, outs, lens = lz4mi.decompress_blocks(bad, caps)
-        for t, c in enumerate(bad):
-            est, ew, eo = O.decompress_block(c, caps[t], js_compat=js)
-            if st[t] == lz4mi.ERR_CROSS_BLOCK:         # batched: reaches before its own block
-                assert not js and est == lz4mi.ERR_DICT_OOB, t   # standalone at offset 0 that is OOB
+            st, outs, lens = lz4mi.decompress_blocks(bad * rep, caps * rep)
+        for t, c in enumerate(bad * rep):
+            est, ew, eo = O.decompress_block(c, caps[t % len(bad)], js_compat=js)
+            t0, t = t, t % len(bad)
+            st_t, out_t, len_t = st[t0], outs[t0], lens[t0]
+            if st_t == lz4mi.ERR_CROSS_BLOCK:          # batched: reaches before its own block
+                assert not js and est == lz4mi.ERR_DICT_OOB, (t0, rep)   # standalone at offset 0 that is OOB
                 continue
-            assert st[t] == est, (t, js)
+            assert st_t == est, (t0, js, rep)
             if est == 0:
-                assert lens[t] == ew, (t, js)
-                assert np.array_equal(outs[t], eo[:min(ew, caps[t])]), (t, js)
+                assert len_t == ew, (t0, js, rep)
+                assert np.array_equal(out_t, eo[:min(ew, caps[t])]), (t0, js, rep)
 
 
 @pytest.mark.parametrize("kind", ["random", "repetitive", "tiles216"])
