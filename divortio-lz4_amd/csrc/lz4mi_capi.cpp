@@ -15,6 +15,8 @@
 #include <mutex>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "../../include/lz4mi.h"
 #include "lz4mi_decompress.h"
 
@@ -171,6 +173,24 @@ uint32_t small_blocks() {
 // `order`: scratch of nblocks words for the dispatch order, owned by the caller's lock
 // (nullptr: the blocks go in index order); `small`: the small-batch path's scratch (nullptr:
 // never taken)
+}  // namespace
+
+// Output memory of the host-pointer entry points is usually fresh (a new Uint8Array from the JS
+// layer): every 4 KiB page faults on its first write, inside the D2H copy. A 16 MiB copy into fresh
+// 4 KiB pages takes 1.79 ms, into 2 MiB pages 0.31 ms, and registering or staging through pinned
+// memory does not help (tools/d2h_options.py, profiles/r05_hostio). The 2 MiB-aligned interior of
+// an output range of at least 4 MiB is advised for transparent huge pages: a hint on the caller's
+// mapping, no change to its contents. LZ4MI_THP=0 leaves the caller's memory alone.
+extern "C" __attribute__((visibility("hidden"))) void lz4mi_advise_output(void* p, uint64_t n) {
+    constexpr uintptr_t kHuge = 2u << 20;
+    const char* e = std::getenv("LZ4MI_THP");
+    if ((e && e[0] == '0') || !p || n < 2 * kHuge) return;
+    const uintptr_t a0 = ((uintptr_t)p + kHuge - 1) & ~(kHuge - 1), a1 = ((uintptr_t)p + n) & ~(kHuge - 1);
+    if (a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
+}
+
+namespace {
+
 hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
@@ -398,6 +418,7 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     }
     uint64_t hist = std::min<uint64_t>(lo, 65536);
     uint64_t base = lo - hist, img = hi - base;
+    lz4mi_advise_output(out + lo, hi - lo);
     std::vector<uint64_t> d_in_off(nblocks), d_out_off(nblocks);
     uint64_t pos = 0;
     for (uint32_t b = 0; b < nblocks; ++b) {
@@ -504,6 +525,13 @@ int32_t lz4mi_compress_blocks(const uint8_t* in, const uint64_t* in_off, const u
                                     m_out_len, nblocks, c->tables.as<int32_t>(), s));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));
+    uint64_t olo = UINT64_MAX, ohi = 0;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        if (out_len[b]) {
+            olo = std::min<uint64_t>(olo, out_off[b]);
+            ohi = std::max<uint64_t>(ohi, out_off[b] + out_len[b]);
+        }
+    if (ohi > olo) lz4mi_advise_output(out + olo, ohi - olo);
     for (uint32_t b = 0; b < nblocks; ++b)
         if (out_len[b])
             LZ4MI_TRY(hipMemcpyAsync(out + out_off[b], g_ctx.out.as<uint8_t>() + d_out_off[b], out_len[b],

@@ -19,6 +19,8 @@
 
 #include "../../include/lz4mi.h"
 
+extern "C" __attribute__((visibility("hidden"))) void lz4mi_advise_output(void* p, uint64_t n);   // (lz4mi_capi.cpp)
+
 namespace {
 
 constexpr uint32_t kMul = 2654435761u;
@@ -286,6 +288,7 @@ extern "C" int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_to
                                                uint32_t dict_len, uint32_t flags) {
     if ((!in && in_total) || (!out && out_total) || (!dict && dict_len) || in_off < 0 || in_size < 0 || out_off < 0)
         return LZ4MI_ERR_ARG;
+    if ((uint64_t)out_off < out_total) lz4mi_advise_output(out + out_off, out_total - (uint64_t)out_off);   // (lz4mi_capi.cpp)
     return decompress_block(Arr{in, (int64_t)in_total}, in_off, in_off + in_size, OutArr{out, (int64_t)out_total},
                             out_off, Arr{dict, (int64_t)dict_len}, !(flags & (LZ4MI_JS_COMPAT | LZ4MI_JS_EXACT)));
 }

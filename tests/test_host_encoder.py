@@ -235,3 +235,24 @@ def test_host_encoder_matches_oracle_fuzz(gen):
                 assert got_n == want_n, (gen, seed, cap)
             assert np.array_equal(got_out, want_out), (gen, seed, cap)
             assert np.array_equal(got_t, want_t), (gen, seed, cap)
+
+
+@pytest.mark.parametrize("thp", ["1", "0"])
+def test_host_decoder_large_fresh_output(thp, monkeypatch):
+    """A block decoded into a fresh (never written) output mapping larger than 4 MiB at an
+    unaligned offset: the library advises the range's 2 MiB-aligned interior for huge pages
+    (lz4mi_advise_output; LZ4MI_THP=0 skips it). Bytes in the output before the offset and past
+    the block stay as they were; the block equals the oracle's decode."""
+    import mmap
+    monkeypatch.setenv("LZ4MI_THP", thp)
+    src = O.generate("tiles216", 77, 9 << 20)
+    comp = O.compress_block_bytes(src)
+    m = mmap.mmap(-1, (12 << 20) + 4096)
+    out = np.frombuffer(m, dtype=np.uint8)
+    off = 4096 + 123
+    out[:off] = 0xA5
+    w = lz4mi.host_decompress_raw(comp, 0, comp.size, out, off, spec=True)
+    assert w == src.size and np.array_equal(out[off:off + w], src)
+    assert (out[:off] == 0xA5).all() and (out[off + w:] == 0).all()
+    del out
+    m.close()
