@@ -8,10 +8,12 @@ const input = new Uint8Array(fs.readFileSync(process.argv[2]));
 const BS = 4194304;
 const now = () => Number(process.hrtime.bigint()) / 1e6;
 const REPS = Number(process.argv[4] || 5);
+const gc = globalThis.gc || (() => {});   // (node --expose-gc: earlier results collected before each call)
 const med = (fn, n = REPS) => {
+    gc();
     fn();
     const ts = [];
-    for (let r = 0; r < n; r++) { const t0 = now(); fn(); ts.push(now() - t0); }
+    for (let r = 0; r < n; r++) { gc(); const t0 = now(); fn(); ts.push(now() - t0); }
     ts.sort((a, b) => a - b);
     return +ts[(n - 1) >> 1].toFixed(3);
 };

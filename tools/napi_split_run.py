@@ -7,7 +7,7 @@ import oracle as O  # noqa: E402
 path = "/tmp/lz4mi_split_%d.bin" % os.getpid()
 np.concatenate([O.generate("tiles216", 1 + i, 4 << 20) for i in range(16)]).tofile(path)
 try:
-    r = subprocess.run(["node", "--no-warnings", os.path.join(ROOT, "tools", "napi_split.mjs"), path] + sys.argv[1:],
+    r = subprocess.run(["node", "--no-warnings", "--expose-gc", os.path.join(ROOT, "tools", "napi_split.mjs"), path] + sys.argv[1:],
                        capture_output=True, text=True, timeout=250)
     print(r.stdout.strip()[-4000:])
     print(r.stderr[-1500:], file=sys.stderr)
