@@ -153,10 +153,10 @@ StreamCtx* stream_ctx(hipStream_t s) {
     return g_ctx.streams.back().get();
 }
 
-// Small batches (at most this many blocks, LZ4 spec or reference mode) decode with 64 waves per
-// block (a segment-parallel parse) and the output by pointer jumping over the whole GPU
-// (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216 block 0.25 ms instead
-// of 7.9. The batch kernel is a flat 8.3 ms up to 4096 tiles216 blocks; the small path grows
+// Small batches (at most this many blocks, LZ4 spec or reference mode) decode with a wave per
+// ~8 KiB of each compressed block (a segment-parallel parse) and the output by pointer jumping
+// over the whole GPU (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216
+// block 0.24 ms instead of 7.9. The batch kernel is a flat 8.3 ms up to 4096 tiles216 blocks; the small path grows
 // ~0.063 ms per block (128 blocks: 8.13 ms, profiles/r06c), so the default is 96 blocks. Blocks
 // of long runs (ratio >= 32) are decoded by one wave in the same launch. LZ4MI_SMALL_BLOCKS=0
 // turns the path off.

@@ -1176,7 +1176,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     const uint32_t nseg = XP ? a.xsegs : 1u;   // XP: waves per block (one per segment)
     if (blockIdx.x >= a.nblocks * nseg) return;
     const uint32_t wblk = XP ? blockIdx.x / nseg : blockIdx.x;   // (XP: block-major, segments of a block on
-    const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;       //  64 consecutive CUs, every XCD)
+    const uint32_t sg = XP ? blockIdx.x - wblk * nseg : 0u;       //  consecutive CUs, every XCD)
     const uint32_t b = a.order ? uniform(a.order[wblk]) : wblk;
     if (!XP && a.redo && !uniform(a.redo[b])) return;   // (small batches, reference mode: the blocks to redo)
 #if LZ4MI_TIMELINE
@@ -1938,10 +1938,11 @@ __global__ __launch_bounds__(64, 4) void lz4mi_decompress_kernel(DecArgs a) { de
 // small batches: a wave per segment of each block, sequences exported (lz4mi_expand.hip)
 __global__ __launch_bounds__(64, 4) void lz4mi_decompress_x_kernel(DecArgs a) { decompress_block<true>(a); }
 
-// Between the two phases of an exported small batch, per block: the segments in order from
-// segment 0 (whose entry is the block's first token): each whose speculative entry equals the
-// previous one's exit is final (fin), and one the chain passes over is empty; xfirst[b] = the
-// first segment that is neither (xsegs: none), re-parsed by phase 1.
+// After phase 0 and after phase 2 of an exported small batch, per block: the segments in order
+// from segment 0 (whose entry is the block's first token): each whose speculative entry equals
+// the previous one's exit is final (fin), and one the chain passes over is empty; xfirst[b] = the
+// first segment that is neither (xsegs: none), where phase 1 starts; and every later segment's
+// re-parse entry for phase 2 (`from`).
 __global__ __launch_bounds__(64) void lz4mi_xverify_kernel(DecArgs a) {
     static_assert(kSegMax == 4 * 64, "four records per lane");
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
