@@ -431,9 +431,19 @@ def c_cpu_baseline(batch, threads, target_s=1.5):
             break
     assert (st == 0).all()
     gbps = reps * nb * BLOCK / el / 1e9
+    # the baseline doubles as a checker of the GPU's results at the bench's scale: its decode of
+    # the GPU-compressed blocks equals the generated bytes, and the oracle encoder's bytes for a
+    # few of those blocks equal the GPU encoder's (compressBlock is deterministic)
+    raw = batch.raw[:nb * BLOCK].cpu().numpy()
+    dec_ok = bool(np.array_equal(out, raw))
+    ncmp = min(nb, 8)
+    comp_ok = all(np.array_equal(O.compress_block_bytes(raw[b * BLOCK:(b + 1) * BLOCK]),
+                                 comp[b * batch.slot:b * batch.slot + int(lens[b])]) for b in range(ncmp))
     return {"value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"oracle C decoder, {nb} x 4 MiB blocks of the same compressed batch, {reps} passes, "
-                      f"{threads} pthreads, {el:.1f} s wall"}
+                      f"{threads} pthreads, {el:.1f} s wall",
+            "oracle_check": {"decoded_equal_generated_blocks": nb, "decoded_ok": dec_ok,
+                             "compressed_equal_oracle_blocks": ncmp, "compressed_ok": bool(comp_ok)}}
 
 
 def napi_e2e(batch, nblocks=128):
