@@ -159,6 +159,7 @@ struct DecShared {
     uint32_t stage[kStageWords];
 };
 static_assert(kLim / 2 >= kMaxSeq, "pending list must fit in the next-token table");
+static_assert(kStageWords * 4 > kLim, "the table build reads s[q + 2] for offsets ending at kLim");
 static_assert(offsetof(DecShared, stage) % 16 == 0 && offsetof(DecShared, pme) % 16 == 0, "16-byte aligned rows");
 
 // LDS a whole-wave periodic run may copy its pattern into, by phase of the
@@ -1478,7 +1479,10 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                     ll[j] = x1 ? 15u + b1[j] : tok[j] >> 4;
                     lit[j] = p[j] + 1 + x1;
                     q[j] = lit[j] + ll[j];
-                    const uint32_t qa = q[j] + 2 < (uint32_t)kLim ? q[j] : 0u;   // (a long literal run: slow below)
+                    // offset bytes inside the window (q + 2 <= kLim: a sequence may end on its last byte,
+                    // as next_token accepts; s[q + 2] is still staged) -- past it only a long literal run
+                    // (slow below)
+                    const uint32_t qa = q[j] + 2 <= (uint32_t)kLim ? q[j] : 0u;
                     o0[j] = s[qa];
                     o1[j] = s[qa + 1];
                     mb[j] = s[qa + 2];

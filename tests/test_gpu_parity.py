@@ -414,3 +414,46 @@ def test_compress_literal_runs_around_ring_size():
     st, outs, lens = lz4mi.decompress_blocks(comps, [b.size for b in blocks])
     for k, (b, o) in enumerate(zip(blocks, outs)):
         assert st[k] == 0 and np.array_equal(o, b), k
+
+
+def _window_edge_stream(end, ll=200, off=100):
+    """An LZ4 block whose sequence with `ll` literals (one extension byte) ends its offset exactly
+    at compressed position `end` (the decoder's first chunk covers [0, 1088)): 8 literals + a
+    4-byte match, 3-byte sequences up to the token, the long sequence, literal-only tail."""
+    out = bytearray([0x80]) + bytes(range(65, 73)) + bytes([8, 0])          # 8 literals, offset 8, ml 4
+    size = 1 + ll - 15                                                       # (token, ext, literals, offset)
+    p = end - (1 + 1 + ll + 2)
+    r = (p - len(out)) % 3                                                   # r 4-byte sequences (1 literal)
+    k = (p - len(out) - 4 * r) // 3
+    assert k >= 0
+    out += bytes([0x10, 0x2A, 4, 0]) * r + bytes([0x00, 4, 0]) * k          # ml 4, offset 4
+    assert len(out) == p
+    out += bytes([0xF0, size - 1]) + bytes((i * 7 + 3) & 255 for i in range(ll)) + bytes([off & 255, off >> 8])
+    assert len(out) == end
+    out += bytes([0x50]) + b"tail!"                                          # the last literals
+    return np.frombuffer(bytes(out), dtype=np.uint8)
+
+
+def test_sequence_ending_on_the_window_edge():
+    """A sequence whose offset's last byte is the last byte of the decoder's 1088-byte window
+    (kLim) is parsed inside the window, and its offset must be read from the window (it was read
+    from the window's first bytes: found by tools/small_fuzz.py); neighbouring alignments too,
+    through the small-batch path, the batch kernel and the reference-compatible kernel."""
+    streams, sizes = [], []
+    for end in (1085, 1086, 1087, 1088, 1089, 1090, 1091):
+        for ll in (17, 200, 269):
+            try:
+                s = _window_edge_stream(end, ll)
+            except AssertionError:
+                continue
+            est, ew, eo = O.decompress_block(s, 1 << 16)
+            assert est == 0
+            streams.append(s)
+            sizes.append(ew)
+    assert any(s.size > 1088 for s in streams)
+    exp = [O.decompress_block(s, n)[2][:n] for s, n in zip(streams, sizes)]
+    for rep in (1, 104 // len(streams) + 1):     # the small-batch path, then the batch kernel
+        st, outs, lens = lz4mi.decompress_blocks(streams * rep, sizes * rep)
+        assert (st == 0).all() and all(np.array_equal(o, exp[i % len(exp)]) for i, o in enumerate(outs)), rep
+    st, outs, lens = lz4mi.decompress_blocks(streams, sizes, js_compat=True)
+    assert (st == 0).all() and all(np.array_equal(o, e) for o, e in zip(outs, exp))

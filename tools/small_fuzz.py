@@ -12,6 +12,7 @@ import lz4mi  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--seconds", type=float, default=60)
 ap.add_argument("--seed", type=int, default=1)
+ap.add_argument("--dump", default="", help="directory: the first mismatching block's input and outputs (.npz), then stop")
 args = ap.parse_args()
 rng = np.random.default_rng(args.seed)
 gens = ["tiles216", "text", "copy", "runs", "random", "repetitive"]
@@ -44,6 +45,12 @@ while time.time() - t0 < args.seconds:
             bad += 1
             print("MISMATCH batch", batches, "block", j, "status", int(st[j]), "oracle", int(est),
                   "len", int(lens[j]), int(ew), flush=True)
+            if args.dump:
+                os.makedirs(args.dump, exist_ok=True)
+                np.savez(os.path.join(args.dump, "mismatch.npz"), comp=c, cap=np.array([caps[j]]), got=outs[j],
+                         want=eo[:min(ew, caps[j])], batch_comps=np.array([x.size for x in comps]), j=np.array([j]))
+                print({"dumped": True, "batch_blocks": len(comps)}, flush=True)
+                sys.exit(1)
     batches += 1
     blocks += k
 print({"mode": os.environ.get("LZ4MI_SMALL_REPARSE", "0"), "batches": batches, "blocks": blocks, "mismatches": bad}, flush=True)
