@@ -1,4 +1,5 @@
 # the window-edge offset fix: the new test against the pre-fix library (must fail) and the fixed one,
+set -o pipefail
 # the GPU suite, the fuzz-found block in every re-parse mode, the small-path stress in every mode
 cd $GRAFT_REPO_ROOT && T=${1:-r05_edge} && mkdir -p gpurun_out/$T
 timeout -k 10 120 python -u tools/run_test_with_so.py tools/variants/liblz4mi_prefix.so test_sequence_ending_on_the_window_edge 2>&1 | grep -v amdgpu.ids | tee gpurun_out/$T/old_lib.log || exit 1
