@@ -455,7 +455,9 @@ def test_sequence_ending_on_the_window_edge():
     for rep in (1, 104 // len(streams) + 1):     # the small-batch path, then the batch kernel
         st, outs, lens = lz4mi.decompress_blocks(streams * rep, sizes * rep)
         assert (st == 0).all() and all(np.array_equal(o, exp[i % len(exp)]) for i, o in enumerate(outs)), rep
-    # reference-compatible mode: the reference's bytes, F1 rewrite included (the 8-offset match)
-    exp_js = [O.decompress_block(s, n, js_compat=True)[2][:n] for s, n in zip(streams, sizes)]
-    st, outs, lens = lz4mi.decompress_blocks(streams, sizes, js_compat=True)
-    assert (st == 0).all() and all(np.array_equal(o, e) for o, e in zip(outs, exp_js))
+    # reference-compatible mode, one block per output array (its positions are absolute in the
+    # array, as test_fuzz_roundtrip_and_corruption does): the reference's bytes, F1 rewrite included
+    for s, n in zip(streams, sizes):
+        est, ew, eo = O.decompress_block(s, n, js_compat=True)
+        st, outs, lens = lz4mi.decompress_blocks([s], [n], js_compat=True)
+        assert st[0] == est == 0 and np.array_equal(outs[0], eo[:n]), s.size
