@@ -138,6 +138,12 @@ class Batch:
                                     self.dec.data_ptr(), self.raw_off.data_ptr(), self.raw_len.data_ptr(),
                                     self.dec_len.data_ptr(), self.status.data_ptr(), self.n, stream)
 
+    def decompress_reference(self, lz4mi, stream):
+        """The same launch with the reference decoder's bytes (LZ4MI_JS_EXACT, the JS layer's default)."""
+        lz4mi.decompress_blocks_dev(self.comp.data_ptr(), self.comp_off.data_ptr(), self.comp_len.data_ptr(),
+                                    self.dec.data_ptr(), self.raw_off.data_ptr(), self.raw_len.data_ptr(),
+                                    self.dec_len.data_ptr(), self.status.data_ptr(), self.n, stream, js_exact=True)
+
     def verify(self, torch, lz4mi, stream):
         """Per-block xxh32 of the decoded bytes == of the generated bytes (GPU)."""
         h1 = torch.zeros(self.n, dtype=torch.int32, device="cuda")
@@ -149,6 +155,75 @@ class Batch:
         torch.cuda.synchronize()
         return bool((self.status == 0).all().item()) and bool(torch.equal(h1, h2)) and \
             bool((self.dec_len == BLOCK).all().item())
+
+
+def reference_mode(torch, lz4mi, batch, stream_obj, gen, seed0, steps=5):
+    """the headline batch decoded with the reference decoder's bytes
+    (LZ4MI_JS_EXACT: the spec kernel plus the in-chunk replay of the double-copy-tail rewrites,
+    SURVEY F1), timed like the headline (HIP events on the launch stream). Checked against the
+    reference's own census of this batch (tests/golden/manifest.json 'bench_batch_js_decode',
+    generated by executing the reference: per-block digests of its decode, each block in an array of
+    its own): every block's XXH32 (GPU) must equal it. A block whose rewrite reaches before its own
+    output reports LZ4MI_ERR_CROSS_BLOCK in the batch and is decoded alone into a scratch block,
+    as the JS layer does (`cross_block_ms`)."""
+    s = stream_obj.cuda_stream
+    _, k = timed(torch, None, lambda: batch.decompress_reference(lz4mi, s), steps, 1, stream_obj)
+    n = batch.n
+    st = batch.status.cpu().tolist()
+    cross = [b for b in range(n) if st[b] == lz4mi.ERR_CROSS_BLOCK]
+    h = torch.zeros(n, dtype=torch.int32, device="cuda")
+    lz4mi.xxh32_blocks_dev(batch.dec.data_ptr(), batch.raw_off.data_ptr(), batch.dec_len.data_ptr(), h.data_ptr(),
+                           n, 0, s)
+    hr = torch.zeros(n, dtype=torch.int32, device="cuda")
+    lz4mi.xxh32_blocks_dev(batch.raw.data_ptr(), batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), hr.data_ptr(),
+                           n, 0, s)
+    torch.cuda.synchronize()
+    h, hr = [int(x) & 0xFFFFFFFF for x in h.tolist()], [int(x) & 0xFFFFFFFF for x in hr.tolist()]
+    lens = batch.dec_len.cpu().tolist()
+    cross_ms = 0.0
+    if cross:
+        one = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+        z64 = torch.zeros(1, dtype=torch.int64, device="cuda")
+        cap = torch.full((1,), BLOCK, dtype=torch.int32, device="cuda")
+        ol, os_ = torch.zeros(1, dtype=torch.int32, device="cuda"), torch.zeros(1, dtype=torch.int32, device="cuda")
+        hh = torch.zeros(1, dtype=torch.int32, device="cuda")
+        for b in cross:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream_obj)
+            lz4mi.decompress_blocks_dev(batch.comp.data_ptr() + b * batch.slot, z64.data_ptr(),
+                                        batch.comp_len.data_ptr() + 4 * b, one.data_ptr(), z64.data_ptr(),
+                                        cap.data_ptr(), ol.data_ptr(), os_.data_ptr(), 1, s, js_exact=True)
+            e1.record(stream_obj)
+            lz4mi.xxh32_blocks_dev(one.data_ptr(), z64.data_ptr(), ol.data_ptr(), hh.data_ptr(), 1, 0, s)
+            torch.cuda.synchronize()
+            cross_ms += e0.elapsed_time(e1)
+            st[b], lens[b], h[b] = int(os_.item()), int(ol.item()), int(hh.item()) & 0xFFFFFFFF
+    ok = all(x == 0 for x in st) and all(x == BLOCK for x in lens)
+    fixed = sum(1 for b in range(n) if h[b] != hr[b])
+    census = None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
+            census = [c for c in json.load(f)["cases"] if c["kind"] == "bench_batch_js_decode"][0]
+    except (OSError, ValueError, IndexError):
+        pass
+    checked = 0
+    if census is not None and gen == "tiles216" and census["gen"] == gen:
+        rows = {r["seed"]: int(r["js_dec_xxh"], 16) for r in census["rows"]}
+        lo, hi = census["seeds"]
+        for b in range(n):
+            sd = seed0 + b
+            if lo <= sd <= hi:
+                ok &= h[b] == rows.get(sd, hr[b])
+                checked += 1
+    comp_bytes = int(batch.comp_len.sum().item())
+    return {"kernel_ms": round(k * 1e3, 3), "GBps": round(n * BLOCK / k / 1e9, 1),
+            "frac": round((n * BLOCK + comp_bytes) / k / 1e9 / HBM_PEAK_GBPS, 4),
+            "blocks_fixed_up": fixed, "cross_block_blocks": len(cross), "cross_block_ms": round(cross_ms, 3),
+            "verified": bool(ok and checked == n), "blocks_checked_vs_reference_census": checked,
+            "note": "LZ4MI_JS_EXACT (the JS layer's default): the reference decoder's bytes, double-copy-tail "
+                    "rewrites (SURVEY F1) included; blocks_fixed_up = blocks whose output differs from their "
+                    "input (the reference's own decode of them differs too); every block's XXH32 checked against "
+                    "the reference's census of seeds 1..4096 (tests/golden, made by executing the reference)"}
 
 
 def mix_order(n):
@@ -587,6 +662,7 @@ def main():
 
     d_wall, d_kern = timed(torch, dist, lambda: batch.decompress(lz4mi, stream), args.steps, args.warmup, stream_obj)
     ok = batch.verify(torch, lz4mi, stream)
+    ref_mode = reference_mode(torch, lz4mi, batch, stream_obj, args.gen, 1 + rank * n) if rank == 0 else None
 
     okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device="cuda")
     if dist is not None:
@@ -677,6 +753,8 @@ def main():
     }
     if traffic_src:
         line["roofline"]["traffic_source"] = traffic_src
+    if ref_mode is not None:
+        line["reference_mode"] = ref_mode
     if world > 1:   # every rank's average launch time: the imbalance the max hides
         line["per_rank_kernel_ms"] = {"decompress": per_rank_ms[0], "compress": per_rank_ms[1]}
     if frame is not None:

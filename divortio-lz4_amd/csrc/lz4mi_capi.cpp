@@ -160,6 +160,13 @@ StreamCtx* stream_ctx(hipStream_t s) {
 // ~0.063 ms per block (128 blocks: 8.13 ms, profiles/r06c), so the default is 96 blocks. Blocks
 // of long runs (ratio >= 32) are decoded by one wave in the same launch. LZ4MI_SMALL_BLOCKS=0
 // turns the path off.
+// Scratch (lz4mi_small_scratch_bytes): ~16 B per potential sequence of the largest compressed
+// block plus 4 B per output byte of the largest output, per block of the batch. Host-pointer calls
+// size it from the batch's real maxima (rounded up to 64 KiB); device-pointer calls cannot read
+// in_len/out_cap without a sync, so they size it for the largest block the path exports (a 4 MiB
+// block: ~47 MB per block). Either way the total is capped (LZ4MI_SMALL_SCRATCH_MB, default 4608 =
+// 96 worst-case blocks): a batch above the cap goes to the batch kernel. A block larger than the
+// sizing is decoded by one wave inside the same launch (the kernel's export limits).
 constexpr uint32_t kSmallInMax = (4u << 20) + (4u << 20) / 255 + 16;   // a 4 MiB block's compress bound
 constexpr uint32_t kSmallOutMax = 4u << 20;
 uint32_t small_blocks() {
@@ -169,10 +176,22 @@ uint32_t small_blocks() {
     }();
     return n;
 }
+size_t small_scratch_cap() {
+    static const size_t n = [] {
+        const char* e = std::getenv("LZ4MI_SMALL_SCRATCH_MB");
+        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4608) << 20;
+    }();
+    return n;
+}
+int small_reparse_hook() {   // (test hook, read per call: LZ4MI_SMALL_REPARSE forces re-parses, tests/test_gpu_small.py)
+    const char* e = std::getenv("LZ4MI_SMALL_REPARSE");
+    return e ? std::atoi(e) : 0;
+}
 
 // `order`: scratch of nblocks words for the dispatch order, owned by the caller's lock
 // (nullptr: the blocks go in index order); `small`: the small-batch path's scratch (nullptr:
-// never taken)
+// never taken); in_max / out_max: the batch's largest compressed block and output capacity when
+// the caller knows them (host pointers), 0 = unknown (device pointers: the path's limits)
 }  // namespace
 
 // Output memory of the host-pointer entry points is usually fresh (a new Uint8Array from the JS
@@ -194,15 +213,25 @@ namespace {
 hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint32_t* out_cap, const uint8_t* dict, uint32_t dict_len,
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
-                         Scratch* order, Scratch* small = nullptr) {
-    if (small && (mode == 0 || mode == 2) && nblocks <= small_blocks() &&
-        small->ensure(lz4mi_small_scratch_bytes(nblocks, kSmallInMax, kSmallOutMax), s) == hipSuccess)
-        return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len,
-                                             status, nblocks, kSmallInMax, kSmallOutMax, small->p,
-                                             std::getenv("LZ4MI_SMALL_REPARSE") ? std::atoi(std::getenv("LZ4MI_SMALL_REPARSE")) : 0,   // (test hook)
-                                             mode == 2 ? 1 : 0, s);
+                         Scratch* order, Scratch* small = nullptr, uint32_t in_max = 0, uint32_t out_max = 0) {
+    if (small && (mode == 0 || mode == 2) && nblocks <= small_blocks()) {
+        constexpr uint32_t kGrain = 64u << 10;
+        const uint32_t xi = in_max ? std::min(kSmallInMax, (in_max + kGrain - 1) / kGrain * kGrain) : kSmallInMax;
+        const uint32_t xo = out_max ? std::min(kSmallOutMax, (out_max + kGrain - 1) / kGrain * kGrain) : kSmallOutMax;
+        const size_t need = lz4mi_small_scratch_bytes(nblocks, xi, xo);
+        if (need <= small_scratch_cap()) {
+            if (small->ensure(need, s) == hipSuccess)
+                return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len,
+                                                     out_len, status, nblocks, xi, xo, small->p, small_reparse_hook(),
+                                                     mode == 2 ? 1 : 0, s);
+            (void)hipGetLastError();   // the failed allocation is not this call's error: the batch kernel runs
+        }
+    }
     uint32_t* ord = nullptr;
-    if (order && nblocks > 1 && order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();
+    if (order && nblocks > 1) {
+        if (order->ensure((size_t)nblocks * 4, s) == hipSuccess) ord = order->as<uint32_t>();
+        else (void)hipGetLastError();   // index order instead
+    }
     return lz4mi_launch_decompress(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status,
                                    nblocks, mode, ord, s);
 }
@@ -452,9 +481,11 @@ int32_t lz4mi_decompress_blocks(const uint8_t* in, const uint64_t* in_off, const
     LZ4MI_TRY(hipMemcpyAsync(m_out_off, d_out_off.data(), 8ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_in_len, in_len, 4ull * nblocks, hipMemcpyHostToDevice, s));
     LZ4MI_TRY(hipMemcpyAsync(m_out_cap, out_cap, 4ull * nblocks, hipMemcpyHostToDevice, s));
+    const uint32_t in_max = *std::max_element(in_len, in_len + nblocks);
+    const uint32_t out_max = *std::max_element(out_cap, out_cap + nblocks);
     LZ4MI_TRY(decode_launch(g_ctx.in.as<uint8_t>(), m_in_off, m_in_len, g_ctx.out.as<uint8_t>(), m_out_off, m_out_cap,
                             dlen ? g_ctx.aux.as<uint8_t>() : nullptr, dlen, m_out_len, m_status, nblocks, mode, s,
-                            &g_ctx.order, &g_ctx.small));
+                            &g_ctx.order, &g_ctx.small, std::max(in_max, 1u), std::max(out_max, 1u)));
     LZ4MI_TRY(hipMemcpyAsync(out_len, m_out_len, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipMemcpyAsync(status, m_status, 4ull * nblocks, hipMemcpyDeviceToHost, s));
     LZ4MI_TRY(hipStreamSynchronize(s));

@@ -482,9 +482,6 @@ __device__ __forceinline__ uint4 ld16(const CompJob& j, int64_t p) {
     return make_uint4(ld_u32(j, p), ld_u32(j, p + 4), ld_u32(j, p + 8), ld_u32(j, p + 12));
 }
 
-#ifndef LZ4MI_DUPSLOT
-#define LZ4MI_DUPSLOT 1   // hit batches test for repeated hashes with an LDS slot before the DPP checks (A/B switch)
-#endif
 // The batch encoder's loads (zero outside the block). 32-bit offsets from the block's scalar
 // base instead were slower (77.9 vs 74.9 ms, round 4).
 __device__ __forceinline__ uint4 ld16o(const CompJob& j, uint32_t lim, int32_t p) {
@@ -662,7 +659,6 @@ __device__ int64_t compress_block_gts(const CompJob& j, SH& F, int32_t* T, int l
                     dup = true;                                        \
                 }                                                      \
             }
-#if LZ4MI_DUPSLOT
             // repeated hashes are rare: a lane-id slot keyed by hash & 1023 finds whether the batch
             // has any (two lanes of one hash always collide; a collision of two hashes only sends
             // the batch through the exact checks below)
@@ -674,9 +670,6 @@ __device__ int64_t compress_block_gts(const CompJob& j, SH& F, int32_t* T, int l
                 anydup = __ballot(act && vs[h & 1023] != (uint8_t)lane) != 0;
             }
             if (anydup) { LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7) }
-#else
-            if (K > 1) { LZ4MI_DUP(1) LZ4MI_DUP(2) LZ4MI_DUP(3) LZ4MI_DUP(4) LZ4MI_DUP(5) LZ4MI_DUP(6) LZ4MI_DUP(7) }
-#endif
 #undef LZ4MI_DUP
             static_assert(kSpecK == 8, "LZ4MI_DUP / LZ4MI_LATER cover distances 1..7");
             const uint32_t litv = npend ? load_lit() : 0u;
@@ -740,11 +733,7 @@ __device__ int64_t compress_block_gts(const CompJob& j, SH& F, int32_t* T, int l
                 const uint32_t hd = dpp<0x100 + d>(0xFFFFFFFFu, h);    \
                 if (lane + d <= J && hd == h) later = true;            \
             }
-#if LZ4MI_DUPSLOT
             if (J > 0 && anydup) { LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7) }
-#else
-            if (J > 0) { LZ4MI_LATER(1) LZ4MI_LATER(2) LZ4MI_LATER(3) LZ4MI_LATER(4) LZ4MI_LATER(5) LZ4MI_LATER(6) LZ4MI_LATER(7) }
-#endif
 #undef LZ4MI_LATER
             insert(lane <= J && !later, h, p);
             const int32_t pJ = lane_val(p, J), cJ = lane_val(cand, J);

@@ -41,15 +41,10 @@
 //     length varints: incompressible or highly repetitive data) is parsed from
 //     global memory with wave-wide 255-run scans and written by the whole
 //     wave, literal run first, then (after it is stored) the match run.
+#include "../../include/lz4mi.h"
 #include "lz4mi_common.h"
 #include "lz4mi_decompress.h"
 
-#ifndef LZ4MI_PERIODIC_LDS
-#define LZ4MI_PERIODIC_LDS 1   // 0: long periodic runs re-read history (A/B switch)
-#endif
-#ifndef LZ4MI_LIT_NT
-#define LZ4MI_LIT_NT 1   // long literal runs copied with nontemporal loads and stores (A/B switch)
-#endif
 #ifndef LZ4MI_LL_ADAPT
 #define LZ4MI_LL_ADAPT 127   // long literal runs: s_sleep argument after every 4 KiB step while blocks with a
                              // compression ratio above 2 run on the same XCD (0: no pacing; A/B switch)
@@ -57,9 +52,6 @@
 #ifndef LZ4MI_ORDER
 #define LZ4MI_ORDER 1   // batches dispatched latency-bound blocks first, most compressed bytes first; 2: the
                         // latency-bound blocks first in index order; 0: index order (A/B switch)
-#endif
-#ifndef LZ4MI_PER_ALIGN
-#define LZ4MI_PER_ALIGN 1   // long periodic runs stored on the 16-byte grid; 0: at the run's own alignment (A/B switch)
 #endif
 #ifndef LZ4MI_ABLATE
 #define LZ4MI_ABLATE 0   // timing-only variants (tools/): 1 = no output, 2 = parse only, 3 = next table only,
@@ -127,19 +119,19 @@ constexpr int kLim = kChunk + kPad;           // chunk-relative bytes a regular 
 constexpr int kStageWords = (kLim + 28) / 4;  // + slack for 16-byte literal loads at the window end
 constexpr int kMaxSeq = kChunk / 3 + 3;       // tokens starting in the chunk: every non-final sequence is >= 3 bytes
 constexpr uint32_t kWarm = 512;               // speculative walks start this far before their segment
-constexpr int kMaxVarint = 250;
-constexpr int32_t LZ4MI_ERR_RANGE_STATUS = -8;   // include/lz4mi.h LZ4MI_ERR_RANGE               // longer length varints go to the cut path (ml < 65536)
+constexpr int kMaxVarint = 250;               // longer length varints go to the cut path (ml < 65536)
+constexpr int32_t LZ4MI_ERR_RANGE_STATUS = LZ4MI_ERR_RANGE;   // (include/lz4mi.h)
 constexpr uint32_t kEnd = 0x40000000u;        // chain ends (last sequence of the block)
 constexpr uint32_t kStop = 0x40000001u;       // sequence cannot be parsed inside the window
 constexpr int kWaveB = 2;                     // ... (whole-wave runs: streaming copies)
 constexpr int kWaveB2 = 1;                    // ... (whole-wave periodic runs: two windows per piece)
 constexpr int kLaneBytes = 256;               // longer runs are written by the whole wave (128: tiles216 +1.8 %)
 constexpr int kPeriodBulk = 1024;             // longer periodic runs are generated from an LDS copy of the pattern
-constexpr int32_t kLongLit = 4096;
+constexpr int32_t kLongLit = 4096;            // literal runs at least this long: long_literals()
 constexpr uint64_t kXRatioMax = 32;           // XP: blocks of higher ratio are decoded by one wave
 constexpr int kSegRestarts = 16;              // XP: a guess's walk starts over at most this often
 constexpr uint32_t kSegWarm = 3072;           // XP: a segment's warm-up parse (tiles216: 99 % of wrong
-                                              // starts join the token chain within 860 bytes)            // literal runs at least this long: long_literals()
+                                              // starts join the token chain within 860 bytes)
 
 struct DecShared {
     union {
@@ -651,9 +643,6 @@ struct WaveGen {
 // the source + kMemoBase when the whole match was mapped (remap_src follows it in one step for
 // later rows), + kSplitBase when only its part after a literal prefix was (0: not mapped).
 constexpr int32_t kMemoBase = 0x40000000, kSplitBase = 0x20000000;
-#ifndef LZ4MI_REMAP_MEMO
-#define LZ4MI_REMAP_MEMO 1   // 0: every hop through the sequences (A/B switch)
-#endif
 
 // A match source [rs, re) inside this table's output, mapped back through the
 // sequences that wrote it (out[y] = out[y - off] inside a match): 1 = it now
@@ -692,7 +681,6 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
             rs = ms;
         }
         if (re > ms + q.ml) return 0;
-#if LZ4MI_REMAP_MEMO
         if (q.rsrc >= kMemoBase - 65536 && q.rsrc < kMemoBase + (1 << 27)) {
             // sequence lo's match was itself mapped (by an earlier row) to finished output:
             // follow that mapping in one step instead of hop by hop
@@ -701,7 +689,6 @@ __device__ __forceinline__ int remap_src(const Ctx& c, const DecShared& S, uint3
             re += base;
             continue;
         }
-#endif
         rs -= q.off;
         re -= q.off;
     }
@@ -890,7 +877,6 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
         }
         __syncthreads();
         // every piece whose phase falls in this slice; the phase is carried from piece to piece
-#if LZ4MI_PER_ALIGN
         // pieces on the absolute 16-byte grid (whole-line stores), the unaligned head piece
         // written once more by lane 0 (same bytes), the last piece overlapping its predecessor
         const int32_t a0 = (int32_t)((0u - (uint32_t)(uintptr_t)(c.dst + R.y)) & 15u);
@@ -913,20 +899,6 @@ __device__ __forceinline__ void periodic_run(const Ctx& c, const DecShared& S, i
             r += step;
             if (r >= per) r -= per;
         }
-#else
-        const int32_t np = run_pieces(R.n);
-        const int32_t step = (16 * kWave) % per;
-        int32_t r = (16 * lane) % per;
-#pragma unroll 1
-        for (int32_t p = lane; p < np; p += kWave) {
-            const bool last = 16 * p > dl;
-            const int32_t d = last ? dl : 16 * p;
-            const int32_t ph = (last ? d % per : r) - s0;
-            if ((uint32_t)ph < (uint32_t)(e0 - s0) && LZ4MI_ABLATE != 4) out16(c.dst + R.y + d, stage16(B.w, ph));
-            r += step;
-            if (r >= per) r -= per;
-        }
-#endif
     }
     __syncthreads();
 }
@@ -953,7 +925,6 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
 #endif
         const int32_t d0 = at(p0), d1 = at(p0 + kWave), d2 = at(p0 + 2 * kWave), d3 = at(p0 + 3 * kWave);
         uint4 v0, v1, v2, v3;
-#if LZ4MI_LIT_NT
         // streamed once, never re-read soon: nontemporal, so they do not evict the history lines
         // other blocks' matches read back from L2
         v0 = ld16_nt(src + d0);
@@ -964,16 +935,6 @@ __device__ __forceinline__ void long_literals(uint8_t* dst, const uint8_t* src, 
         st16_nt(dst + d1, v1);
         st16_nt(dst + d2, v2);
         st16_nt(dst + d3, v3);
-#else
-        __builtin_memcpy(&v0, src + d0, 16);
-        __builtin_memcpy(&v1, src + d1, 16);
-        __builtin_memcpy(&v2, src + d2, 16);
-        __builtin_memcpy(&v3, src + d3, 16);
-        out16(dst + d0, v0);
-        out16(dst + d1, v1);
-        out16(dst + d2, v2);
-        out16(dst + d3, v3);
-#endif
 #if LZ4MI_LL_ADAPT
         if (busy) __builtin_amdgcn_s_sleep(LZ4MI_LL_ADAPT);
 #endif
@@ -986,7 +947,7 @@ __device__ __forceinline__ void wave_run(const Ctx& c, DecShared& S, int lane, c
     // (a byte-wise periodic run whose source is inside the buffer qualifies too:
     // periodic_run reads only [src, src + period))
     const bool in_buf = R.kind == R_HIST || (R.kind == R_BYTES && c.out_off + R.src >= 0);
-    if (LZ4MI_PERIODIC_LDS && in_buf && R.period && R.n > kPeriodBulk &&
+    if (in_buf && R.period && R.n > kPeriodBulk &&
         B.bytes > 0 && (R.period + 48 <= B.bytes || (R.n >= 4 * R.period && B.bytes >= 1024))) {
         periodic_run(c, S, lane, R, B);
         return;

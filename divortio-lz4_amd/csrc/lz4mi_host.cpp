@@ -13,6 +13,7 @@
 // typed array drops them, and the RangeError output.set() throws for a literal run of
 // more than 64 bytes that does not fit (blockCompress.js:100, :198).
 #include <climits>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -288,7 +289,12 @@ extern "C" int64_t lz4mi_host_decompress_block(const uint8_t* in, uint64_t in_to
                                                uint32_t dict_len, uint32_t flags) {
     if ((!in && in_total) || (!out && out_total) || (!dict && dict_len) || in_off < 0 || in_size < 0 || out_off < 0)
         return LZ4MI_ERR_ARG;
-    if ((uint64_t)out_off < out_total) lz4mi_advise_output(out + out_off, out_total - (uint64_t)out_off);   // (lz4mi_capi.cpp)
+    // only the range this block can write: a length byte adds at most 255 output bytes, so a block of
+    // in_size bytes writes fewer than 255 * in_size + 64 (a caller decoding block after block into
+    // one large array does not advise the whole rest of it on every call)
+    if ((uint64_t)out_off < out_total)
+        lz4mi_advise_output(out + out_off, std::min<uint64_t>(out_total - (uint64_t)out_off,
+                                                              255ull * (uint64_t)in_size + 64));   // (lz4mi_capi.cpp)
     return decompress_block(Arr{in, (int64_t)in_total}, in_off, in_off + in_size, OutArr{out, (int64_t)out_total},
                             out_off, Arr{dict, (int64_t)dict_len}, !(flags & (LZ4MI_JS_COMPAT | LZ4MI_JS_EXACT)));
 }

@@ -342,12 +342,13 @@ def xxh32_blocks(blocks, seed=0, standard=False):
 # handle (int, e.g. torch.cuda.current_stream().cuda_stream). Async.
 def decompress_blocks_dev(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr, out_len_ptr,
                           status_ptr, nblocks, stream=0, js_compat=False, dict_ptr=None, dict_len=0,
-                          frame_words=False):
+                          frame_words=False, js_exact=False):
     """Batch decode on device pointers. frame_words: in_len holds frame size words (bit 31 =
-    stored block, copied in the same launch; include/lz4mi.h LZ4MI_FRAME_WORDS)."""
+    stored block, copied in the same launch; include/lz4mi.h LZ4MI_FRAME_WORDS). js_exact: the
+    reference decoder's bytes (LZ4MI_JS_EXACT, the JS layer's default)."""
     _check(lib().lz4mi_decompress_blocks(in_ptr, in_off_ptr, in_len_ptr, out_ptr, out_off_ptr, out_cap_ptr,
                                          dict_ptr, dict_len, out_len_ptr, status_ptr, nblocks,
-                                         DEVICE_PTRS | (JS_COMPAT if js_compat else 0) |
+                                         DEVICE_PTRS | _dec_flags(js_compat, js_exact) |
                                          (FRAME_WORDS if frame_words else 0), stream or None))
 
 

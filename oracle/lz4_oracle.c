@@ -523,10 +523,10 @@ static void* mt_worker(void* arg) {
     mt_job_t* j = (mt_job_t*)arg;
     int32_t* table = (int32_t*)malloc(16384 * sizeof(int32_t));
     for (uint32_t b = j->tid; b < j->nblocks; b += j->nthreads) {
-        if (j->mode == 0) {
+        if (j->mode == 0 || j->mode == 2) {
             int64_t w = 0;
             int32_t st = orc_decompress_block(j->in + j->in_off[b], j->in_len[b], 0, j->in_len[b],
-                                              j->out + j->out_off[b], j->out_cap[b], 0, NULL, 0, 0, &w);
+                                              j->out + j->out_off[b], j->out_cap[b], 0, NULL, 0, j->mode == 2, &w);
             j->status[b] = st; j->out_len[b] = (uint32_t)w;
         } else {
             memset(table, 0, 16384 * sizeof(int32_t));
@@ -539,7 +539,9 @@ static void* mt_worker(void* arg) {
     return NULL;
 }
 
-/* mode 0 = decompress, 1 = compress (fresh table per block). Independent
+/* mode 0 = decompress (spec), 1 = compress (fresh table per block), 2 = decompress with the
+ * reference decoder's bytes (js_compat: the F1 double-copy tail, blockDecompress.js:234-249),
+ * each block in an output array of its own (nothing before its offset 0). Independent
  * blocks spread round-robin over `nthreads` pthreads. */
 int32_t orc_blocks_mt(int32_t mode, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                       uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap, uint32_t* out_len,

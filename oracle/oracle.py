@@ -197,7 +197,8 @@ def decompress_frame(frame, dictionary=None, verify_checksum=True, js_compat=Fal
 
 
 def blocks_mt(mode, inp, in_off, in_len, out, out_off, out_cap, nthreads):
-    """Multi-threaded CPU pass over independent blocks (mode 0 decompress, 1 compress)."""
+    """Multi-threaded CPU pass over independent blocks (mode 0 decompress, 1 compress,
+    2 decompress with the reference decoder's bytes, js_compat)."""
     n = len(in_len)
     out_len = np.zeros(n, dtype=np.uint32)
     status = np.zeros(n, dtype=np.int32)
@@ -205,3 +206,36 @@ def blocks_mt(mode, inp, in_off, in_len, out, out_off, out_cap, nthreads):
                         out_off.ctypes.data, out_cap.ctypes.data, out_len.ctypes.data, status.ctypes.data,
                         n, nthreads)
     return out_len, status
+
+
+def census(kind, seed0, nblocks, bs, nthreads, js_compat=True, chunk=256):
+    """Per block b (seed seed0 + b): xxh32 of the generated bytes, the compressed length and its xxh32
+    (the oracle encoder, fresh table), and the decode's status, length and xxh32 (the reference decoder's
+    bytes with js_compat, each block in an array of its own). Host threads, `chunk` blocks at a time."""
+    from concurrent.futures import ThreadPoolExecutor
+    res = {k: [] for k in ("src_xxh", "comp_len", "comp_xxh", "dec_status", "dec_len", "dec_xxh")}
+    cap = compress_bound(bs)
+    with ThreadPoolExecutor(nthreads) as ex:     # the C calls drop the GIL
+        for b0 in range(0, nblocks, chunk):
+            k = min(chunk, nblocks - b0)
+            host = np.concatenate(list(ex.map(lambda b: generate(kind, seed0 + b, bs), range(b0, b0 + k))))
+            res["src_xxh"] += list(ex.map(lambda j: xxh32(host[j * bs:(j + 1) * bs]), range(k)))
+            in_off = np.arange(k, dtype=np.uint64) * bs
+            in_len = np.full(k, bs, dtype=np.uint32)
+            comp = np.zeros(k * cap, dtype=np.uint8)
+            c_off = np.arange(k, dtype=np.uint64) * cap
+            c_cap = np.full(k, cap, dtype=np.uint32)
+            clen, _ = blocks_mt(1, host, in_off, in_len, comp, c_off, c_cap, nthreads)
+            res["comp_len"] += [int(x) for x in clen]
+            res["comp_xxh"] += list(ex.map(lambda j: xxh32(comp[j * cap:j * cap + int(clen[j])]), range(k)))
+            host[:] = 0
+            dlen, dst = blocks_mt(2 if js_compat else 0, comp, c_off, clen, host, in_off, in_len, nthreads)
+            res["dec_status"] += [int(x) for x in dst]
+            res["dec_len"] += [int(x) for x in dlen]
+            res["dec_xxh"] += list(ex.map(lambda j: xxh32(host[j * bs:j * bs + int(dlen[j])]), range(k)))
+    return res
+
+
+def digest_of_digests(hashes):
+    """XXH32 over the u32 digests, little-endian, in order (tests/golden 'bench_batch_js_decode')."""
+    return xxh32(np.array([h & 0xFFFFFFFF for h in hashes], dtype="<u4").view(np.uint8))

@@ -404,3 +404,31 @@ def test_frame_decompress_on_device_matches_reference():
     with pytest.raises(lz4mi.Lz4miError) as ei:
         F.decompress_frame_device(bad)
     assert str(ei.value) == "LZ4: Invalid Magic Number"
+
+
+def test_js_exact_tiles216_f1_blocks_match_reference_census(manifest):
+    """tiles216 4 MiB blocks whose reference decode differs from their input (the reference's census
+    of the bench batch, tests/golden section 12): seeds 33 and 62 and two with a single
+    rewritten 4-byte group, batched with two F1-free seeds and one at a time, in reference mode
+    (LZ4MI_JS_EXACT) == the reference decoder's digest; in spec mode == the input."""
+    (g,) = cases_of(manifest, "bench_batch_js_decode")
+    rows = {r["seed"]: r for r in g["rows"]}
+    seeds = [33, 62, 969, 1426, 1, 2]
+    bs = g["n"]
+    srcs = [O.generate("tiles216", sd, bs) for sd in seeds]
+    comps = [O.compress_block_bytes(x) for x in srcs]
+    for sd, c in zip(seeds, comps):
+        if sd in rows:
+            assert c.size == rows[sd]["comp_len"] and "%08x" % O.xxh32(c) == rows[sd]["comp_xxh"]
+    want = ["%08x" % (int(rows[sd]["js_dec_xxh"], 16) if sd in rows else O.xxh32(x)) for sd, x in zip(seeds, srcs)]
+    st, outs, lens = lz4mi.decompress_blocks(comps, [bs] * len(seeds), js_exact=True)
+    for k, sd in enumerate(seeds):
+        if st[k] == lz4mi.ERR_CROSS_BLOCK:
+            continue
+        assert st[k] == 0 and lens[k] == bs and "%08x" % O.xxh32(outs[k]) == want[k], sd
+    for k, (sd, c) in enumerate(zip(seeds, comps)):
+        out = np.zeros(bs, dtype=np.uint8)
+        assert lz4mi.decompress_raw(c, 0, c.size, out, 0, js_exact=True) == bs
+        assert "%08x" % O.xxh32(out) == want[k], sd
+        out[:] = 0
+        assert lz4mi.decompress_raw(c, 0, c.size, out, 0) == bs and np.array_equal(out, srcs[k]), sd

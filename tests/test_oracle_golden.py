@@ -268,3 +268,22 @@ def test_block_checksum_frames_interoperate_with_liblz4():
         # the reference-style reader skips them and decodes the same bytes
         st, back = O.decompress_frame(f)
         assert st == 0 and np.array_equal(back, data)
+
+
+def test_oracle_reference_decode_of_the_bench_batch(manifest):
+    """The headline batch (tiles216 seeds 1..4096, 4 MiB) under the reference decoder: the
+    reference's own census (gen_golden.mjs section 12: 116 of 4096 blocks decode differently from
+    their input, SURVEY F1) pins the oracle's js_compat decode. Seeds 1..512 here (12 F1 blocks);
+    the GPU test (test_gpu_parity.py) runs all 4096 against both."""
+    (g,) = cases_of(manifest, "bench_batch_js_decode")
+    assert g["seeds"] == [1, 4096] and len(g["rows"]) == 116
+    rows = {r["seed"]: r for r in g["rows"]}
+    n = 512
+    r = O.census("tiles216", 1, n, g["n"], 8)
+    assert all(st == 0 for st in r["dec_status"]) and all(w == g["n"] for w in r["dec_len"])
+    for s in range(1, n + 1):
+        want = rows[s]["js_dec_xxh"] if s in rows else "%08x" % r["src_xxh"][s - 1]
+        assert "%08x" % r["dec_xxh"][s - 1] == want, s
+        if s in rows:
+            assert r["comp_len"][s - 1] == rows[s]["comp_len"] and "%08x" % r["comp_xxh"][s - 1] == rows[s]["comp_xxh"]
+    assert sum(1 for s in rows if s <= n) == 12

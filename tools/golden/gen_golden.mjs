@@ -356,6 +356,40 @@ for (const [name, src, genSpec] of blockInputs) {
         dec_equals_input: back.ok && back.value.length === x.length && back.value.every((v, i) => v === x[i]) });
 }
 
+// ---- 12. the bench batch under the reference decoder (BASELINE configs[1], VERDICT r5 item 1) ----
+{
+    // The headline batch is tiles216 seeds 1..4096 at 4 MiB. Its double-copy-tail rewrites (SURVEY F1)
+    // change ~2 % of those blocks under the reference's decompressBlock, each block decoded into an
+    // array of its own. Pinned here for every seed: the rows of the blocks whose reference decode
+    // differs from the input (with their digests), and one XXH32 over all 4096 decode digests
+    // (LE u32 each, in seed order), so the GPU's reference mode is checked against the reference
+    // itself at the bench's full scale. No bytes are kept.
+    const N = 4194304, SEEDS = 4096;
+    const out = new Uint8Array(N + (N / 255 | 0) + 16);
+    const dec = new Uint8Array(N);
+    const all = new Uint8Array(4 * SEEDS);
+    const rows = [];
+    for (let seed = 1; seed <= SEEDS; seed++) {
+        const src = gen('tiles216', seed, N);
+        const n = compressBlock(src, out, 0, N, new Int32Array(16384), 0);
+        dec.fill(0);
+        const w = decompressBlock(out, 0, n, dec, 0);
+        const h = xxHash32(dec) >>> 0;
+        all[4 * (seed - 1)] = h & 255; all[4 * (seed - 1) + 1] = (h >>> 8) & 255;
+        all[4 * (seed - 1) + 2] = (h >>> 16) & 255; all[4 * (seed - 1) + 3] = (h >>> 24) & 255;
+        let same = w === N;
+        for (let i = 0; same && i < N; i++) if (dec[i] !== src[i]) same = false;
+        if (!same) {
+            let first = 0; while (first < N && dec[first] === src[first]) first++;
+            let diff = 0; for (let i = 0; i < N; i++) if (dec[i] !== src[i]) diff++;
+            rows.push({ seed, comp_len: n, comp_xxh: hex(xxHash32(out.subarray(0, n))), src_xxh: hex(xxHash32(src)),
+                js_dec_written: w, js_dec_xxh: hex(h), first_diff: first, bytes_differ: diff });
+        }
+    }
+    manifest.cases.push({ kind: 'bench_batch_js_decode', gen: 'tiles216', seeds: [1, SEEDS], n: N, rows,
+        js_dec_xxh_of_digests: hex(xxHash32(all)) });
+}
+
 fs.writeFileSync(path.join(OUT, 'manifest.json'), JSON.stringify(manifest, null, 1));
 console.log('wrote', manifest.cases.length, 'case groups to', OUT);
 }
