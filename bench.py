@@ -325,7 +325,7 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
     return {
         "workload": f"LZ4 frame (independent 4 MiB blocks, content size + content xxh32), {n} tiles216 blocks "
                     f"per rank x {world} rank(s) = {total_raw / 2**30:.0f} GiB; assembled on rank 0, then decoded "
-                    f"sharded (contiguous block runs) and gathered back to rank 0 (BASELINE.json configs[3])",
+                    f"sharded (contiguous block runs of equal decode cost) and gathered back to rank 0 (BASELINE.json configs[3])",
         "raw_bytes": total_raw, "frame_bytes": int(fbytes.item()), "verified": bool(ok.item()),
         "compress": {"kernel_ms": ms(ck), "kernel_collective_ms": ms(c_coll),
                      "checksum_chain_ms": ms(tc.get("checksum_chain", 0.0)),

@@ -162,7 +162,7 @@ StreamCtx* stream_ctx(hipStream_t s) {
 // turns the path off.
 // Scratch (lz4mi_small_scratch_bytes): ~16 B per potential sequence of the largest compressed
 // block plus 4 B per output byte of the largest output, per block of the batch. Host-pointer calls
-// size it from the batch's real maxima (rounded up to 64 KiB); device-pointer calls cannot read
+// size it from the batch's real maxima (rounded up to 64 KiB, the output's to a power of two); device-pointer calls cannot read
 // in_len/out_cap without a sync, so they size it for the largest block the path exports (a 4 MiB
 // block: ~47 MB per block). Either way the total is capped (LZ4MI_SMALL_SCRATCH_MB, default 4608 =
 // 96 worst-case blocks): a batch above the cap goes to the batch kernel. A block larger than the
@@ -215,9 +215,12 @@ hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32
                          uint32_t* out_len, int32_t* status, uint32_t nblocks, int mode, hipStream_t s,
                          Scratch* order, Scratch* small = nullptr, uint32_t in_max = 0, uint32_t out_max = 0) {
     if (small && (mode == 0 || mode == 2) && nblocks <= small_blocks()) {
+        // (the output limit is a power of two: lz4mi_launch_expand tiles it)
         constexpr uint32_t kGrain = 64u << 10;
         const uint32_t xi = in_max ? std::min(kSmallInMax, (in_max + kGrain - 1) / kGrain * kGrain) : kSmallInMax;
-        const uint32_t xo = out_max ? std::min(kSmallOutMax, (out_max + kGrain - 1) / kGrain * kGrain) : kSmallOutMax;
+        uint32_t xo = kGrain;
+        while (xo < out_max && xo < kSmallOutMax) xo <<= 1;
+        if (!out_max) xo = kSmallOutMax;
         const size_t need = lz4mi_small_scratch_bytes(nblocks, xi, xo);
         if (need <= small_scratch_cap()) {
             if (small->ensure(need, s) == hipSuccess)

@@ -633,7 +633,8 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
 
     frame: the whole frame on root (1-D uint8 tensor; a CUDA tensor is indexed and scattered
     on the device), ignored on the other ranks. Root indexes the size words, every rank gets
-    the index (broadcast) and a contiguous run of blocks — the frame bytes of its run, sent
+    the index (broadcast) and a contiguous run of blocks of about equal decode cost
+    (shard.balanced_runs) — the frame bytes of its run, sent
     point to point (RCCL over xGMI for CUDA tensors) — decodes them in one batch on its
     device, and the outputs are gathered to root in block order (`gather`), else each rank
     returns its own part. The content checksum (FLG 0x04) is verified on root's host from
@@ -698,10 +699,12 @@ def decompress_frame_sharded(frame, verify_checksum=True, group=None, root=0, de
         dist.broadcast(pay, src=src, group=group)
         dist.broadcast(word, src=src, group=group)
     t0 = _phase(timings, "index", t0, dev, group)
-    # ---- contiguous runs of blocks: rank r's frame bytes [a_r, b_r)
+    # ---- contiguous runs of blocks of about equal decode cost (shard.balanced_runs): rank r's
+    # frame bytes [a_r, b_r)
     bsum = 4 if flg & 0x10 else 0
     size = word & 0x7FFFFFFF
-    runs = [shard.shard_range(nb, r, world) for r in range(world)]
+    word_h = word.tolist()
+    runs = shard.balanced_runs(word_h, bmax, world)
     pay_h, size_h = pay.tolist(), size.tolist()
 
     def span(lo, hi):

@@ -432,3 +432,45 @@ def test_js_exact_tiles216_f1_blocks_match_reference_census(manifest):
         assert "%08x" % O.xxh32(out) == want[k], sd
         out[:] = 0
         assert lz4mi.decompress_raw(c, 0, c.size, out, 0) == bs and np.array_equal(out, srcs[k]), sd
+
+
+def test_frame_past_4gib():
+    """a frame whose compressed bytes exceed 2^32 (configs[3] at 8 GPUs is ~8.6 GB):
+    1280 x 4 MiB blocks, 7 of 8 random (stored records) and every 8th tiles216 (compressed, some past the
+    4 GiB mark), through compress_frame_sharded (content checksum) and decompress_frame_sharded (index,
+    scatter, batch decode with stored blocks in the same launch, checksum verified) and the single-GPU
+    device frame path; payload positions past 2^32 in the index, the content checksum equal to the
+    oracle's XXH32 of the raw bytes, the last compressed block equal to the oracle encoder's."""
+    from lz4mi import frame as F
+    n = 1280
+    raw = torch.empty(n * BLOCK, dtype=torch.uint8, device="cuda")
+    lz4mi.generate_blocks_dev(raw.data_ptr(), "random", 7000, BLOCK, n, _stream())
+    tiles = [b for b in range(n) if b % 8 == 7]
+    tmp = torch.empty(BLOCK, dtype=torch.uint8, device="cuda")
+    for b in tiles:
+        lz4mi.generate_blocks_dev(tmp.data_ptr(), "tiles216", 9000 + b, BLOCK, 1, _stream())
+        raw[b * BLOCK:(b + 1) * BLOCK].copy_(tmp)
+    del tmp
+    torch.cuda.synchronize()
+    frame = F.compress_frame_sharded(raw, BLOCK, content_checksum=True, add_content_size=True)
+    torch.cuda.synchronize()
+    assert frame.numel() > (1 << 32)
+    meta, pay, word = F.frame_index(frame)
+    assert pay.numel() == n and meta["content_size"] == n * BLOCK and int(pay[-1]) > (1 << 32)
+    stored = ((word & 0x80000000) != 0).cpu().numpy()
+    assert stored.sum() == n - len(tiles) and not stored[tiles].any()
+    # the content checksum (the frame's last 4 bytes) == the oracle's XXH32 of all raw bytes
+    host = raw.cpu().numpy()
+    assert int.from_bytes(frame[-4:].cpu().numpy().tobytes(), "little") == O.xxh32(host)
+    # the last compressed record (past 2^32) == the oracle encoder's bytes
+    b = tiles[-1]
+    p, w = int(pay[b]), int(word[b])
+    assert p > (1 << 32)
+    want = O.compress_block_bytes(host[b * BLOCK:(b + 1) * BLOCK])
+    assert w == want.size and np.array_equal(frame[p:p + w].cpu().numpy(), want)
+    del host
+    back = F.decompress_frame_sharded(frame, verify_checksum=True)
+    assert back.numel() == n * BLOCK and torch.equal(back, raw)
+    del back
+    dev = F.decompress_frame_device(frame, verify_checksum=True)
+    assert dev.numel() == n * BLOCK and torch.equal(dev, raw)

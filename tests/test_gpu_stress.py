@@ -109,3 +109,75 @@ def test_encoder_stress():
         comps = lz4mi.compress_blocks(srcs)
         for j, (s, c) in enumerate(zip(srcs, comps)):
             assert np.array_equal(c, O.compress_block_bytes(s)), (j, s.size)
+
+
+
+def _seg_geom(in_len):
+    """csrc/lz4mi_decompress.h seg_geom: S segments of L compressed bytes (the small path's waves)."""
+    s = max(1, min(256, -(-in_len // 8192)))
+    L = max(4096, (-(-in_len // s) + 1023) & ~1023)
+    return s, L
+
+
+def _ext(v):
+    return 0 if v < 15 else 1 + (v - 15) // 255
+
+
+def _boundary_stream(rng, comp_len):
+    """A valid LZ4 block of exactly comp_len compressed bytes whose sequences straddle the small path's
+    segment starts k*L (seg_geom) and warm-up starts k*L - 3072: before each such mark a filler sequence
+    puts the next token 0..6 bytes before it, so the mark falls on a token, a literal length byte, a
+    literal, an offset byte or a match length byte. Returns (compressed, decoded size, marks placed)."""
+    S, L = _seg_geom(comp_len)
+    marks = sorted({m for k in range(1, S) for m in (k * L, k * L - 3072) if 64 < m < comp_len - 1200})
+    out, produced, placed = bytearray(), 0, 0
+
+    def seq(ll, ml, off):
+        mc = ml - 4
+        return bytes([(min(ll, 15) << 4) | min(mc, 15)] + (_len_field(ll) if ll >= 15 else [])) + \
+            rng.integers(0, 256, ll, dtype=np.uint8).tobytes() + bytes([off & 255, off >> 8]) + \
+            (bytes(_len_field(mc)) if mc >= 15 else b"")
+
+    def add(ll, ml):
+        nonlocal produced
+        off = int(rng.choice([1, 3, 8, 17, int(rng.integers(1, 65536))]))
+        out.extend(seq(ll, ml, max(1, min(off, produced + ll, 65535))))
+        produced += ll + ml
+
+    add(16, 4)
+    for m in marks:
+        t = m - int(rng.integers(0, 7))          # the next token's position
+        while t - len(out) > 700:                # ordinary sequences up to near the mark
+            add(int(rng.choice([0, 1, 3, 15, 40, 200])), int(rng.choice([4, 16, 19, 64, 120, 300, 1000])))
+        gap = t - len(out)                       # a filler of exactly `gap` bytes: 3 + ext(ll) + ll (ml < 19)
+        ll = next((x for x in range(gap - 3, -1, -1) if x + _ext(x) == gap - 3), None)
+        if ll is None:
+            continue
+        add(ll, int(rng.integers(4, 19)))
+        placed += 1
+        add(int(rng.choice([0, 15, 300])), int(rng.choice([4, 19, 270, 600])))   # the straddling sequence
+    while comp_len - len(out) > 250:
+        add(int(rng.choice([0, 3, 40])) if comp_len - len(out) > 300 else 0, int(rng.choice([4, 64, 300])))
+    ll = comp_len - len(out) - 2                 # the final literal run: 1 + 1 + ll bytes (15 <= ll <= 269)
+    out.extend(bytes([0xF0] + _len_field(ll)) + rng.integers(0, 256, ll, dtype=np.uint8).tobytes())
+    assert len(out) == comp_len
+    return np.frombuffer(bytes(out), dtype=np.uint8), produced + ll, placed
+
+
+@pytest.mark.parametrize("force", [0, 1, 2])
+def test_small_path_segment_boundaries(force, monkeypatch):
+    """random valid streams whose sequences straddle the small path's segment starts
+    and 3 KiB warm-up starts (every field of a sequence on the mark, 0..6 bytes of slack), in the three
+    re-parse modes (LZ4MI_SMALL_REPARSE 0: the guesses as they come, 1: every guess past segment 0 wrong
+    in phase 0, 2: in phases 0 and 2), spec and reference mode, statuses and bytes == the oracle's."""
+    monkeypatch.setenv("LZ4MI_SMALL_REPARSE", str(force))
+    rng = np.random.default_rng(40 + force)
+    comps, caps, placed = [], [], 0
+    for n in [20000, 65536, 131071, 300000, 700001]:
+        c, m, p = _boundary_stream(rng, n)
+        comps.append(c)
+        caps.append(m)
+        placed += p
+    assert placed >= 100
+    _check(comps, caps, js_exact=False)
+    _check(comps, caps, js_exact=True)

@@ -313,3 +313,77 @@ def test_weak_scaling_value_formula_world2():
         assert abs(value - 2 * 8 * (4 << 20) * 5 / max(walls) / 1e9) < 1e-6
         assert per_rank[0] == [round(k * 1e3, 3) for k in kerns]
     assert kerns[0] == kerns[1]          # interleaving gave both ranks the same mix
+
+
+def test_balanced_runs_cover_and_balance():
+    """shard.balanced_runs: contiguous runs covering every block once, in order, each rank's
+    decode cost (shard.block_cost) within one block of an equal share; on a clustered mix (stored
+    random blocks first) the first rank takes the cheap blocks plus some chains."""
+    from lz4mi import shard
+    bmax = 4 << 20
+    for n in (0, 1, 7, 16, 4096):
+        words = [(bmax | 0x80000000) if b < n // 2 else 520000 for b in range(n)]
+        for w in (1, 2, 3, 8):
+            runs = shard.balanced_runs(words, bmax, w)
+            assert len(runs) == w and runs[0][0] == 0 and runs[-1][1] == n
+            assert all(runs[r][1] == runs[r + 1][0] and runs[r][0] <= runs[r][1] for r in range(w - 1))
+            costs = [sum(shard.block_cost(words[b], bmax) for b in range(lo, hi)) for lo, hi in runs]
+            assert max(costs) - min(costs) <= 1.0 + 1e-9 or n < w
+    words = [(bmax | 0x80000000)] * 2048 + [520000] * 2048
+    (a0, b0), (a1, b1) = shard.balanced_runs(words, bmax, 2)
+    assert b0 - a0 > 2048 > b1 - a1 and b0 - a0 == 2048 + 768
+
+
+class _CountingDecoder(_OracleDecoder):
+    def __init__(self):
+        self.blocks = 0
+
+    def decode(self, rng, pay_rel, word, block_max, last_cap):
+        self.blocks += pay_rel.numel()
+        return super().decode(rng, pay_rel, word, block_max, last_cap)
+
+
+def _balanced_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "oracle"), os.path.join(root, "divortio-lz4_amd")]
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from lz4mi import frame as F
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        bs = 65536
+        data = np.concatenate([O.generate("random", 70 + b, bs) for b in range(16)] +
+                              [O.generate("tiles216", 90 + b, bs) for b in range(16)])
+        ref = O.compress_frame(data, None, bs, True, True, True)
+        dec = _CountingDecoder()
+        back = F.decompress_frame_sharded(torch.from_numpy(ref.copy()) if rank == 0 else None, True, decoder=dec)
+        ok = (back is not None and np.array_equal(back.numpy(), data)) if rank == 0 else back is None
+        part = F.decompress_frame_sharded(torch.from_numpy(ref.copy()) if rank == 0 else None, True,
+                                          decoder=_CountingDecoder(), gather=False)
+        q.put((rank, ok, dec.blocks, int(part.numel())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), 0, 0))
+
+
+def test_balanced_sharded_decode_of_clustered_mix_world2():
+    """a clustered mix frame (16 stored random blocks, then 16 tiles216) decoded
+    sharded over 2 gloo ranks: cost-balanced contiguous runs give rank 0 the 16 stored blocks and 6
+    chains (22 blocks) and rank 1 10 chains, instead of 16 + 16; the gathered output is the input and
+    the un-gathered parts are the runs' bytes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_balanced_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True for r in res), res
+    assert [r[2] for r in res] == [22, 10]
+    assert [r[3] for r in res] == [22 * 65536, 10 * 65536]
