@@ -1808,14 +1808,24 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
 #endif
         PROF(7);
         if (a.f1check) {
-            wait_vmem();    // this chunk's stores are complete before they are read back
-            uint32_t dv = 0;
+            // candidates first, from the sequence table alone (offset >= 8, length < 8): a chunk
+            // without one -- every tiles216 chunk -- neither drains its stores here nor reads
+            // them back, so they keep draining beside the next chunk's parse as in spec mode
+            bool cand = false;
             for (uint32_t k = lane; k < nseq; k += kWave) {
                 const SeqInfo q = seq_info(S, k);
-                dv |= f1_changes(c, q.out + q.ll, q.off, q.ml);
+                cand |= q.ml != 0 && q.ml < 8 && q.off >= 8;
             }
-            if (__ballot(dv & 2u)) { status = -9; break; }
-            if (__ballot(dv)) f1_fixup(c, S, lane, nseq, false, 0, 0, 0);
+            if (__ballot(cand)) {
+                wait_vmem();    // this chunk's stores are complete before they are read back
+                uint32_t dv = 0;
+                for (uint32_t k = lane; k < nseq; k += kWave) {
+                    const SeqInfo q = seq_info(S, k);
+                    dv |= f1_changes(c, q.out + q.ll, q.off, q.ml);
+                }
+                if (__ballot(dv & 2u)) { status = -9; break; }
+                if (__ballot(dv)) f1_fixup(c, S, lane, nseq, false, 0, 0, 0);
+            }
         }
 #if LZ4MI_ABLATE == 0 || LZ4MI_ABLATE >= 4
         // the cut sequence's match, after the table's F1 replay (it reads the replayed
@@ -1827,7 +1837,7 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
                 wait_vmem();    // everything below the match is read back as history
                 wave_run(c, S, lane, M, pat_all(S));
             }
-            if (a.f1check) {    // its own tail rewrite, after its copy as in the reference
+            if (a.f1check && cml != 0 && cml < 8 && coff >= 8) {    // its own tail rewrite, after its copy as in the reference
                 wait_vmem();
                 const uint32_t dv = lane == 0 ? f1_changes(c, (int32_t)(tab_hi + cll), (int32_t)coff, (int32_t)cml) : 0u;
                 if (__ballot(dv & 2u)) { status = -9; break; }
