@@ -12,11 +12,12 @@ cp $C/*.h $C/*.hip $C/*.cpp $T/
 F0=${FILE:-lz4mi_decompress.hip}
 [ -n "$SRCFILE" ] && cp "$SRCFILE" $T/$F0   # a whole replacement source for $F0 (e.g. from git show)
 sed -i "$expr" $T/$F0
+sed -i 's|"../../include/lz4mi.h"|"lz4mi.h"|' $T/*.hip $T/*.cpp $T/*.h   # (the copies sit outside the tree)
 mkdir -p $R/tools/variants
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include $*"
 objs=""
 for f in lz4mi_decompress.hip lz4mi_expand.hip lz4mi_decompress_serial.hip lz4mi_compress.hip lz4mi_xxh32.hip lz4mi_frame.hip lz4mi_capi.cpp lz4mi_host.cpp; do
-  if [ "$f" = "$F0" ]; then srcf=$T/$f; else srcf=$C/$f; fi
+  srcf=$T/$f
   /opt/rocm/bin/hipcc $F -c -o $T/$f.o $srcf & objs="$objs $T/$f.o"
 done
 wait
