@@ -223,7 +223,11 @@ hipError_t decode_launch(const uint8_t* in, const uint64_t* in_off, const uint32
         if (!out_max) xo = kSmallOutMax;
         const size_t need = lz4mi_small_scratch_bytes(nblocks, xi, xo);
         if (need <= small_scratch_cap()) {
-            if (small->ensure(need, s) == hipSuccess)
+            // (test hook, read per call: LZ4MI_TEST_SCRATCH_EXTRA_MB asks for that much more, so that the
+            // allocation really fails -- tests/test_gpu_small.py::test_small_batch_scratch_allocation_failure)
+            const char* xe = std::getenv("LZ4MI_TEST_SCRATCH_EXTRA_MB");
+            const size_t extra = xe ? (size_t)std::strtoull(xe, nullptr, 10) << 20 : 0;
+            if (small->ensure(need + extra, s) == hipSuccess)
                 return lz4mi_launch_decompress_small(in, in_off, in_len, out, out_off, out_cap, dict, dict_len,
                                                      out_len, status, nblocks, xi, xo, small->p, small_reparse_hook(),
                                                      mode == 2 ? 1 : 0, s);

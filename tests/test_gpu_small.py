@@ -5,10 +5,14 @@ reference's decompressBlock, blockDecompress.js:55-272): bytes, lengths and stat
 generator (incl. long offset-1 runs, far copies), history before the output offset and
 dictionaries, corrupted streams, and a batch mixing exported blocks with one past the export
 limit (decoded by the same launch as usual)."""
+import os
+
 import numpy as np
 import pytest
 
 import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 lz4mi = pytest.importorskip("lz4mi")
 
@@ -223,3 +227,33 @@ def test_small_batch_reference_mode_matches_reference_decoder():
             assert st[j] == est and lens[j] == ew, (sel, i, st[j], est)
             if est == 0:
                 assert np.array_equal(outs[j], eo[:ew]), (sel, i)
+
+
+def test_small_batch_scratch_allocation_failure():
+    """when the small path's scratch cannot be allocated (here a real hipMalloc failure: the
+    test hook LZ4MI_TEST_SCRATCH_EXTRA_MB asks for a petabyte more), the call falls back to the batch
+    kernel and returns LZ4MI_OK with the right bytes (the failed allocation's error is not the call's);
+    with LZ4MI_SMALL_SCRATCH_MB=0 (the cap) the batch kernel runs too. Each in a fresh process: the cap
+    is read once per process."""
+    import subprocess
+    import sys
+    code = r"""
+import os, sys
+sys.path[:0] = [os.path.join(%r, "oracle"), os.path.join(%r, "divortio-lz4_amd")]
+import numpy as np, oracle as O, lz4mi
+lz4mi.init(0)
+srcs = [O.generate(k, 60 + i, n) for i, (k, n) in enumerate([("tiles216", 1 << 20), ("text", 300000), ("random", 70000)])]
+comps = [O.compress_block_bytes(x) for x in srcs]
+for rep in range(2):
+    st, outs, lens = lz4mi.decompress_blocks(comps, [x.size for x in srcs])
+    assert (st == 0).all() and all(np.array_equal(o, x) for o, x in zip(outs, srcs))
+    for c, x in zip(comps, srcs):      # reference mode, one block per output array
+        st, outs, lens = lz4mi.decompress_blocks([c], [x.size], js_exact=True)
+        est, ew, eo = O.decompress_block(c, x.size, js_compat=True)
+        assert st[0] == est == 0 and lens[0] == ew and np.array_equal(outs[0], eo[:x.size])
+print("ok")
+""" % (ROOT, ROOT)
+    for env in ({"LZ4MI_TEST_SCRATCH_EXTRA_MB": str(1 << 30)}, {"LZ4MI_SMALL_SCRATCH_MB": "0"}):
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-1500:])
