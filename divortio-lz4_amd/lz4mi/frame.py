@@ -293,6 +293,13 @@ class ContentChecksum:
             self.route = "send"
             return
         self.route = "shm"
+        if self.rank == root:    # abort markers of this process's earlier calls
+            import glob
+            for f in glob.glob(os.path.join(_shm_dir(), f"lz4mi_stage_{os.getpid()}_*.abort")):
+                try:
+                    os.unlink(f)
+                except OSError:
+                    pass
         _stage_calls[0] += 1
         tag = torch.tensor([os.getpid(), _stage_calls[0]], dtype=torch.int64, device=dev)
         dist.broadcast(tag, src=self._g(root), group=group)
@@ -323,14 +330,23 @@ class ContentChecksum:
 
     def abort(self):
         """Stop the chain after an error between start() and finish() (no collectives): the
-        thread ends at its next poll, and this call's staging files of this rank (all ranks'
-        on root) are removed."""
+        thread ends at its next poll or staging piece (a writer stops between pieces and writes
+        no marker), and this call's staging files of this rank (all ranks' on root) are removed."""
         self.cancel = True
+        if self.route == "shm" and self.rank == self.root:
+            # the other ranks' writers may still be copying: a marker tells them to stop between
+            # pieces and remove their own file; the files of ranks already done are removed here
+            # (zero bytes, removed by root's next ContentChecksum)
+            with open(self._path(self.root, ".abort"), "w"):
+                pass
         if getattr(self, "thread", None) is not None:
             self.thread.join()
         if self.route == "shm":
             for r in (range(self.world) if self.rank == self.root else [self.rank]):
                 for suf in ("", ".done", ".err", ".done.tmp", ".err.tmp"):
+                    if r != self.rank and suf == "" and not (os.path.exists(self._path(r, ".done")) or
+                                                             os.path.exists(self._path(r, ".err"))):
+                        continue   # still being written: its writer removes it on seeing the marker
                     try:
                         os.unlink(self._path(r, suf))
                     except OSError:
@@ -390,10 +406,16 @@ class ContentChecksum:
                 self.digest = w.digest()
             return
         n = shard.numel()
+        marker = ".err"
         try:
             if n:
                 mm = np.memmap(self._path(self.rank), dtype=np.uint8, mode="w+", shape=(n,))
                 for p in range(0, n, _STAGE_PIECE):
+                    # abort() on this rank, or on root (its marker): stop between pieces, leave no files
+                    if self.cancel or os.path.exists(self._path(self.root, ".abort")):
+                        del mm
+                        marker = None
+                        raise RuntimeError("lz4mi: content checksum aborted")
                     m = min(_STAGE_PIECE, n - p)
                     torch.from_numpy(mm[p:p + m]).copy_(shard[p:p + m])
                 mm.flush()
@@ -402,13 +424,13 @@ class ContentChecksum:
         except BaseException:
             if os.path.exists(self._path(self.rank)):
                 os.unlink(self._path(self.rank))
-            marker = ".err"
             raise
         finally:
-            tmp = self._path(self.rank, marker + ".tmp")
-            with open(tmp, "w") as f:
-                f.write(marker)
-            os.rename(tmp, self._path(self.rank, marker))
+            if marker is not None and not self.cancel and not os.path.exists(self._path(self.root, ".abort")):
+                tmp = self._path(self.rank, marker + ".tmp")
+                with open(tmp, "w") as f:
+                    f.write(marker)
+                os.rename(tmp, self._path(self.rank, marker))
 
     def finish(self):
         """Join the background chain; raises on every rank if any rank failed. Returns the

@@ -387,3 +387,58 @@ def test_balanced_sharded_decode_of_clustered_mix_world2():
     assert all(r[1] is True for r in res), res
     assert [r[2] for r in res] == [22, 10]
     assert [r[3] for r in res] == [22 * 65536, 10 * 65536]
+
+
+def _abort_worker(rank, world, port, q):
+    import glob
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "oracle"), os.path.join(root, "divortio-lz4_amd")]
+    import torch
+    import torch.distributed as dist
+    from lz4mi import frame as F
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        F._STAGE_PIECE = 4096                           # many pieces: the writer is still copying at abort()
+        shard = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, 8 << 20, dtype=np.uint8))
+        ck = F.ContentChecksum(shard.numel(), torch.device("cpu"))
+        ok = ck.route == "shm"
+        ck.start(shard)
+        time.sleep(0.05)
+        if rank == 0:
+            ck.abort()                                  # root's error path: no collective; rank 1 still copying
+        dist.barrier()
+        if rank == 1:
+            ck.thread.join()                            # rank 1's writer saw root's marker and stopped
+            ok = ok and ck.error is not None and "aborted" in str(ck.error)
+        time.sleep(0.2)                                 # a writer that ignored cancel would recreate files now
+        left = [x for x in glob.glob(os.path.join(F._shm_dir(), f"lz4mi_stage_{ck.tag[0]}_{ck.tag[1]}_*"))
+                if not x.endswith(".abort")]
+        q.put((rank, ok, sorted(os.path.basename(x) for x in left)))
+        dist.barrier()
+        if rank == 0:                                   # (root's zero-byte abort marker)
+            for x in glob.glob(os.path.join(F._shm_dir(), f"lz4mi_stage_{ck.tag[0]}_{ck.tag[1]}_*.abort")):
+                os.unlink(x)
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), []))
+
+
+def test_content_checksum_abort_leaves_no_staging_files_world2():
+    """ContentChecksum.abort() on root while the other rank is still copying its shard
+    into /dev/shm (only root aborts, as when root's kernel fails): the writer sees root's abort marker,
+    stops between pieces, removes its file and writes no done/err marker, so no staging file of that
+    call is left behind."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_abort_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True for r in res), res
+    assert all(r[2] == [] for r in res), res
