@@ -640,8 +640,12 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist_mod
+        # (rehearsal hook: LZ4MI_BENCH_SHARE_GPU=1 puts every rank on the GPUs there are, round robin, so the
+        # multi-rank path runs on a 1-GPU box; LZ4MI_BENCH_BACKEND picks the process group backend)
+        if os.environ.get("LZ4MI_BENCH_SHARE_GPU") == "1":
+            local %= torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist_mod.init_process_group(os.environ.get("LZ4MI_BENCH_BACKEND", "nccl"), device_id=torch.device("cuda", local))
         dist = dist_mod
     else:
         torch.cuda.set_device(0)
