@@ -13,7 +13,7 @@ from concurrent.futures import ThreadPoolExecutor
 with ThreadPoolExecutor(16) as ex:
     np.concatenate(list(ex.map(lambda b: O.generate("tiles216", 1 + b, 4 << 20), range(n)))).tofile(path)
 try:
-    for rep in range(2):
+    for rep in range(int(sys.argv[3]) if len(sys.argv) > 3 else 2):
         for tree in (ROOT, os.path.abspath(other)):
             r = subprocess.run(["node", "--no-warnings", "--expose-gc", os.path.join(tree, "tools", "napi_e2e.mjs"), path, "3"],
                                capture_output=True, text=True, timeout=600)
