@@ -181,3 +181,31 @@ def test_small_path_segment_boundaries(force, monkeypatch):
     assert placed >= 100
     _check(comps, caps, js_exact=False)
     _check(comps, caps, js_exact=True)
+
+
+def test_global_table_encoder_on_large_blocks_of_every_generator():
+    """The batch encoder above kLdsTableMaxBlocks (768) keeps its tables in global memory, 15-bit entries
+    with 2-bit epoch codes in LDS relabelled every 32 KiB (csrc/lz4mi_compress.hip). The bench batch
+    covers it with 4 MiB tiles216 blocks and the stress tool with blocks of <= 96 KiB; here 4 MiB blocks
+    of every generator (and a copy of far windows, and a block with a period just under 64 KiB, whose matches sit at the window edge across every
+    epoch edge) go through it in one batch beside 770 tiny blocks: compressed bytes == the oracle's
+    compressBlock, byte for byte, and the round trip decodes."""
+    rng = np.random.default_rng(7)
+    big = [O.generate(g, 31 + k, 4 << 20) for k, g in enumerate(GENS + ["copy", "text"])]
+    far = np.empty(4 << 20, dtype=np.uint8)
+    far[:65536] = rng.integers(0, 256, 65536, dtype=np.uint8)
+    pos = 65536
+    while pos < far.size:
+        ln = min(int(rng.integers(8192, 49152)), far.size - pos)
+        src = pos - int(rng.integers(ln, 65536))
+        far[pos:pos + ln] = far[src:src + ln]
+        pos += ln
+    per = np.resize(rng.integers(0, 256, 65533, dtype=np.uint8), 4 << 20)
+    big += [far, per]
+    tiny = [O.generate("text", 900 + k, int(rng.integers(0, 300))) for k in range(770)]
+    srcs = big + tiny
+    comps = lz4mi.compress_blocks(srcs)
+    for j, (s, c) in enumerate(zip(srcs, comps)):
+        assert np.array_equal(c, O.compress_block_bytes(s)), (j, s.size)
+    st, outs, _ = lz4mi.decompress_blocks(comps[:len(big)], [s.size for s in big])
+    assert (st == 0).all() and all(np.array_equal(o, s) for o, s in zip(outs, big))
