@@ -39,6 +39,7 @@ def block(n):
 
 
 t0, batches, blocks, bad = time.time(), 0, 0, 0
+t_log = t0
 while time.time() - t0 < args.seconds:
     if args.big:
         k = int(rng.integers(769, 901))
@@ -56,5 +57,8 @@ while time.time() - t0 < args.seconds:
             np.save(os.path.join(ROOT, "gpurun_out", f"enc_mismatch_{args.seed}_{batches}_{j}.npy"), s)
     batches += 1
     blocks += k
+    if time.time() - t_log > 30:   # progress (a run longer than 3 minutes must keep writing)
+        t_log = time.time()
+        print({"batches": batches, "blocks": blocks, "mismatches": bad}, flush=True)
 print({"big": args.big, "batches": batches, "blocks": blocks, "mismatches": bad}, flush=True)
 sys.exit(1 if bad else 0)

@@ -66,6 +66,7 @@ for t in range(24):   # a pool of compressed blocks, reused with fresh corruptio
         s = O.generate(gens[t % len(gens)], 500 + t, n)
         pool.append((s, O.compress_block_bytes(s)))
 t0, batches, blocks, bad = time.time(), 0, 0, 0
+t_log = t0
 while time.time() - t0 < args.seconds:
     k = int(rng.integers(args.min_blocks, args.max_blocks + 1))
     sel = rng.integers(0, len(pool), k)
@@ -104,6 +105,9 @@ while time.time() - t0 < args.seconds:
                 sys.exit(1)
     batches += 1
     blocks += k
+    if time.time() - t_log > 30:   # progress (a run longer than 3 minutes must keep writing)
+        t_log = time.time()
+        print({"batches": batches, "blocks": blocks, "mismatches": bad}, flush=True)
 print({"mode": os.environ.get("LZ4MI_SMALL_REPARSE", "0"), "blocks_range": [args.min_blocks, args.max_blocks],
        "js_exact": args.js_exact, "random_streams": args.random_streams, "batches": batches, "blocks": blocks, "mismatches": bad}, flush=True)
 sys.exit(1 if bad else 0)
