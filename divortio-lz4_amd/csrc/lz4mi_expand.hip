@@ -8,13 +8,14 @@
 //   expand: every output byte x gets a source pointer: a literal byte -> its position in the
 //           compressed block (resolved), a match byte -> x - offset, an earlier output byte
 //           (unresolved) or a byte before the block (caller's history / dictionary: resolved);
-//   jump:   ptr[x] = ptr[ptr[x]] for every unresolved x, in place, round after round (10 rounds,
-//           then each pointer left is followed to its end: lz4mi_chase_kernel); each
-//           round at least doubles the hops a pointer has taken, so a chain of D matches is
-//           resolved in ceil(log2 D) + 1 rounds (tiles216: D <= 332, 10 rounds; text: 21 489, 16;
-//           a byte of an overlapping match points into the period before the match, so every
-//           hop lands in an earlier sequence: D < 2^20 sequences of a <= 4 MiB block, 21
-//           rounds). Pointers only point
+//   jump:   ptr[x] = ptr[ptr[x]], five times over in one round (kGathers), for every unresolved
+//           x, in place; two such rounds, then each pointer left is followed to its end
+//           (lz4mi_chase_kernel). Each step at least doubles the hops a pointer has taken, so a
+//           round multiplies them by 32 (tiles216: D <= 332 matches deep, copy 3 329, text
+//           21 489 -- a byte of an overlapping match points into the period before the match,
+//           so every hop lands in an earlier sequence). Five steps per round instead of one
+//           step in each of 10 rounds: each pointer is read and written twice instead of 10
+//           times (small batches 12-27 % faster, round 6, profiles/r06j). Pointers only point
 //           backwards and every value on a chain resolves to the same byte, so reading a
 //           pointer another thread has just replaced (or not yet) is correct either way;
 //   gather: out[x] = the byte the resolved pointer names.
@@ -35,7 +36,11 @@ constexpr uint32_t kLit = 0x80000000u;     // kLit | p: byte p of the compressed
 constexpr uint32_t kHist = 0xC0000000u;    // kHist | (y + 65536): byte y < 0 before the block
 constexpr int kXThreads = 256;
 constexpr int kXBytes = 16;                // output bytes per thread (a wave: 1 KiB)
-constexpr int kJumpRounds = 10;          // doubling rounds; then lz4mi_chase_kernel follows what is left
+#ifndef LZ4MI_JUMP_GATHERS
+#define LZ4MI_JUMP_GATHERS 5   // (A/B, profiles/r06j: 1, 2, 3, 4, 5 and 10 steps per round)
+#endif
+constexpr int kGathers = LZ4MI_JUMP_GATHERS;   // pointer hops per round (each round multiplies a chain's hops by 2^kGathers)
+constexpr int kJumpRounds = (10 + kGathers - 1) / kGathers;   // rounds; then lz4mi_chase_kernel follows what is left
 
 struct ExpArgs {
     const uint8_t* in;
@@ -299,7 +304,10 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r)
 #pragma unroll
         for (int k = 0; k < kXBytes; ++k) v[k] = wbase + lane + 64 * k < n ? P[64 * k] : kLit;
 #pragma unroll
-        for (int k = 0; k < kXBytes; ++k) v[k] = v[k] < kUnres ? Q[v[k]] : v[k];
+        for (int g = 0; g < kGathers; ++g) {
+#pragma unroll
+            for (int k = 0; k < kXBytes; ++k) v[k] = v[k] < kUnres ? Q[v[k]] : v[k];
+        }
 #pragma unroll
         for (int k = 0; k < kXBytes; ++k) {
             if (wbase + lane + 64 * k < n) P[64 * k] = v[k];
@@ -313,8 +321,8 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r)
     if (sm && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(sm)) a.flags[r + 1] = 1u;
 }
 
-// After the doubling rounds: every pointer still unresolved is followed to its end (a chain
-// deeper than 2^kJumpRounds sequences: text 21 489 -> at most 21 more hops).
+// After the jump rounds: every pointer still unresolved is followed to its end (a chain deeper
+// than 2^(kGathers * kJumpRounds) = 1 024 sequences: text 21 489 -> at most 21 more hops).
 __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
   if (a.flags[kJumpRounds] == 0) return;
   X_TILES(a) {

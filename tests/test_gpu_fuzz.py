@@ -108,11 +108,11 @@ def _random_stream(rng, target):
 @pytest.mark.parametrize("path", ["small", "batch"])
 def test_decoder_random_stream_fuzz(path):
     """Random valid streams (every length-field shape, offsets 1..65535, overlapping copies)
-    through the small-batch path (96 blocks) and the batch kernel (104: past the small path's
-    limit), equal to the oracle's decode."""
+    through the small-batch path (lz4mi.SMALL_BLOCKS blocks) and the batch kernel (8 more: past the
+    small path's limit), equal to the oracle's decode."""
     rng = np.random.default_rng(55)
     streams, sizes = [], []
-    for t in range(96 if path == "small" else 104):
+    for t in range(lz4mi.SMALL_BLOCKS if path == "small" else lz4mi.SMALL_BLOCKS + 8):
         target = int(rng.choice([20, 300, 4096, 70000, 500000, 1 << 20]))
         s, n = _random_stream(rng, target)
         streams.append(s)

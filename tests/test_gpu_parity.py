@@ -193,9 +193,9 @@ def test_fuzz_roundtrip_and_corruption():
                 c[rng.integers(0, c.size)] = rng.integers(0, 256)
         bad.append(c)
         caps.append(srcs[t].size + (t % 3) * 7)
-    # spec mode as 48 blocks (the small-batch path) and as the same blocks three times (144: the
-    # batch kernel); reference-compatible mode one block at a time
-    for js, rep in ((False, 1), (False, 3), (True, 1)):
+    # spec mode as 48 blocks (the small-batch path) and as the same blocks repeated past the small
+    # path's limit (the batch kernel); reference-compatible mode one block at a time
+    for js, rep in ((False, 1), (False, lz4mi.SMALL_BLOCKS // 48 + 1), (True, 1)):
         if js:     # one output array per block (see test_decompress_reference_blocks_spec_and_jscompat)
             res = [lz4mi.decompress_blocks([c], [k], js_compat=True) for c, k in zip(bad, caps)]
             st = [r[0][0] for r in res]
@@ -470,7 +470,7 @@ def test_sequence_ending_on_the_window_edge():
             sizes.append(ew)
     assert any(s.size > 1088 for s in streams)
     exp = [O.decompress_block(s, n)[2][:n] for s, n in zip(streams, sizes)]
-    for rep in (1, 104 // len(streams) + 1):     # the small-batch path, then the batch kernel
+    for rep in (1, (lz4mi.SMALL_BLOCKS + 8) // len(streams) + 1):     # the small-batch path, then the batch kernel
         st, outs, lens = lz4mi.decompress_blocks(streams * rep, sizes * rep)
         assert (st == 0).all() and all(np.array_equal(o, exp[i % len(exp)]) for i, o in enumerate(outs)), rep
     # reference-compatible mode, one block per output array (its positions are absolute in the

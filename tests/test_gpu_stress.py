@@ -69,7 +69,8 @@ def test_decode_stress(path, source):
             s = O.generate(GENS[t % len(GENS)], 700 + t, n)
             pool.append((O.compress_block_bytes(s), s.size))
     for it in range(3):
-        k = int(rng.integers(1, 97)) if path == "small" else int(rng.integers(97, 131))
+        lim = lz4mi.SMALL_BLOCKS
+        k = int(rng.integers(1, lim + 1)) if path == "small" else int(rng.integers(lim + 1, lim + 35))
         comps, caps = [], []
         for i in rng.integers(0, len(pool), k):
             c, m = pool[int(i)]
