@@ -10,12 +10,15 @@
 //           (unresolved) or a byte before the block (caller's history / dictionary: resolved);
 //   jump:   ptr[x] = ptr[ptr[x]], five times over in one round (kGathers), for every unresolved
 //           x, in place; two such rounds, then each pointer left is followed to its end
-//           (lz4mi_chase_kernel). Each step at least doubles the hops a pointer has taken, so a
-//           round multiplies them by 32 (tiles216: D <= 332 matches deep, copy 3 329, text
-//           21 489 -- a byte of an overlapping match points into the period before the match,
-//           so every hop lands in an earlier sequence). Five steps per round instead of one
-//           step in each of 10 rounds: each pointer is read and written twice instead of 10
-//           times (small batches 12-27 % faster, round 6, profiles/r06j). Pointers only point
+//           (lz4mi_chase_kernel). A step adds at least the hops the pointer it reads had when
+//           the round began (the steps of one round are not synchronised across threads; most
+//           reads see pointers already advanced in this round), so a round multiplies a
+//           pointer's hops by at least 6 and usually far more (tiles216: chains up to 332
+//           matches deep, copy 3 329, text 21 489 -- a byte of an overlapping match points into
+//           the period before the match, so every hop lands in an earlier sequence). Five steps
+//           per round instead of one step in each of 10 rounds: each pointer is read and written
+//           twice instead of 10 times (small batches 12-27 % faster, round 6, profiles/r06j;
+//           more rounds instead of the chase: slower, profiles/r06r). Pointers only point
 //           backwards and every value on a chain resolves to the same byte, so reading a
 //           pointer another thread has just replaced (or not yet) is correct either way;
 //   gather: out[x] = the byte the resolved pointer names.
@@ -321,8 +324,8 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_jump_kernel(ExpArgs a, int r)
     if (sm && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(sm)) a.flags[r + 1] = 1u;
 }
 
-// After the jump rounds: every pointer still unresolved is followed to its end (a chain deeper
-// than 2^(kGathers * kJumpRounds) = 1 024 sequences: text 21 489 -> at most 21 more hops).
+// After the jump rounds: every pointer still unresolved is followed to its end (chains the two
+// rounds did not finish: at 64 blocks 0.44 ms of a tiles216 decode, 3.1 ms of a text one).
 __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
   if (a.flags[kJumpRounds] == 0) return;
   X_TILES(a) {
