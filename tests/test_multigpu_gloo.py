@@ -400,13 +400,15 @@ def _abort_worker(rank, world, port, q):
     from lz4mi import frame as F
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        F._STAGE_PIECE = 4096                           # many pieces: the writer is still copying at abort()
-        shard = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, 8 << 20, dtype=np.uint8))
+        F._STAGE_PIECE = 1024                           # 65 536 pieces: the writer is still copying at abort()
+        shard = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, 64 << 20, dtype=np.uint8))
         ck = F.ContentChecksum(shard.numel(), torch.device("cpu"))
         ok = ck.route == "shm"
         ck.start(shard)
-        time.sleep(0.05)
         if rank == 0:
+            t_wait = time.time() + 60
+            while not os.path.exists(ck._path(1)) and time.time() < t_wait:
+                time.sleep(0.001)                       # rank 1's writer has started its staging file
             ck.abort()                                  # root's error path: no collective; rank 1 still copying
         dist.barrier()
         if rank == 1:
