@@ -347,9 +347,9 @@ def frame_workload(torch, dist, lz4mi, stream_obj, world, rank, blocks_per_rank)
     }
 
 
-def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 64, 96, 128, 160, 256, 2048, 4096), reps=3):
+def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 64, 128, 192, 256, 2048, 4096), reps=3):
     """device-resident time (HIP events on the launch stream, median of `reps`)
-    of the first b blocks of the headline batch, decode and compress. Decode of <= 160 blocks takes
+    of the first b blocks of the headline batch, decode and compress. Decode of <= 192 blocks takes
     the small-batch path (a wave per ~8 KiB segment: segment-parallel parse, output by pointer jumping,
     csrc/lz4mi_expand.hip); larger batches the batch kernel (one wave per block, every block
     resident: the time is one block's chain latency under the CU's contention). Compress is one

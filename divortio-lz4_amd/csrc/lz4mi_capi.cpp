@@ -156,31 +156,31 @@ StreamCtx* stream_ctx(hipStream_t s) {
 // Small batches (at most this many blocks, LZ4 spec or reference mode) decode with a wave per
 // ~8 KiB of each compressed block (a segment-parallel parse) and the output by pointer jumping
 // over the whole GPU (lz4mi_expand.hip) instead of one wave per block: a lone 4 MiB tiles216
-// block 0.22 ms instead of 7.9. The batch kernel is a flat 8.35 ms up to 4096 tiles216 blocks; the small path grows
-// ~0.043 ms per block (160 blocks: 7.27 ms, 192: 8.63; text 160 blocks 25 ms against 154, profiles/r06k), so the
-// default is 160 blocks. Blocks
+// block 0.21 ms instead of 7.9. The batch kernel is a flat 8.4 ms up to 4096 tiles216 blocks; the small path grows
+// ~0.03 ms per block (192 blocks: 5.7 ms, 256: 7.8, 320: 9.2; the 50/50 mix 6.3 / 8.4 / 10.4 against 8.3; text
+// 192 blocks 18 ms against 153, profiles/r06k2), so the default is 192 blocks. Blocks
 // of long runs (ratio >= 32) are decoded by one wave in the same launch. LZ4MI_SMALL_BLOCKS=0
 // turns the path off.
 // Scratch (lz4mi_small_scratch_bytes): ~16 B per potential sequence of the largest compressed
 // block plus 4 B per output byte of the largest output, per block of the batch. Host-pointer calls
 // size it from the batch's real maxima (rounded up to 64 KiB, the output's to a power of two); device-pointer calls cannot read
 // in_len/out_cap without a sync, so they size it for the largest block the path exports (a 4 MiB
-// block: ~47 MB per block). Either way the total is capped (LZ4MI_SMALL_SCRATCH_MB, default 7680 =
-// 160 worst-case blocks): a batch above the cap goes to the batch kernel. A block larger than the
+// block: ~47 MB per block). Either way the total is capped (LZ4MI_SMALL_SCRATCH_MB, default 9216 =
+// 192 worst-case blocks): a batch above the cap goes to the batch kernel. A block larger than the
 // sizing is decoded by one wave inside the same launch (the kernel's export limits).
 constexpr uint32_t kSmallInMax = (4u << 20) + (4u << 20) / 255 + 16;   // a 4 MiB block's compress bound
 constexpr uint32_t kSmallOutMax = 4u << 20;
 uint32_t small_blocks() {
     static const uint32_t n = [] {
         const char* e = std::getenv("LZ4MI_SMALL_BLOCKS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 160u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 192u;
     }();
     return n;
 }
 size_t small_scratch_cap() {
     static const size_t n = [] {
         const char* e = std::getenv("LZ4MI_SMALL_SCRATCH_MB");
-        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)7680) << 20;
+        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)9216) << 20;
     }();
     return n;
 }

@@ -75,8 +75,12 @@ struct ExpArgs {
 constexpr uint32_t kTile = kXThreads * kXBytes;
 constexpr uint32_t kXGrid = 1u << 17;   // (2048: 8-10 % slower on tiles216, profiles/r06e)
 #define X_TILES(a) for (uint32_t tile_ = blockIdx.x; tile_ < (a).ntiles; tile_ += gridDim.x)
-#define X_B(a) (tile_ >> (a).tshift)                  // (x_out_max / kTile: a power of two)
-#define X_T(a) (tile_ & ((1u << (a).tshift) - 1u))
+// Tile-major: tile t of every block before tile t + 1 of any, so the waves dispatched first hold the
+// early output of every block. Pointers point backwards, so a later tile's rounds (and its chase) read
+// pointers the earlier tiles have already advanced. Block-major order (every tile of block 0 first)
+// took 34 % longer on tiles216 at 64 and 160 blocks, and 40 % longer on text (round 6, profiles/r06t).
+#define X_B(a) (tile_ % ((a).ntiles >> (a).tshift))   // (ntiles >> tshift = the batch's blocks)
+#define X_T(a) (tile_ / ((a).ntiles >> (a).tshift))
 // This thread's 16 output bytes [x0, x0 + 16) of tile t of block b, and n = the block's
 // output length (0: nothing to do here)
 __device__ __forceinline__ uint32_t x_span(const ExpArgs& a, uint32_t b, uint32_t t, uint32_t& x0) {

@@ -85,7 +85,7 @@ function blockId(bytes) {             // bufferCompress.js:77-82
 // PCIe copies, and the host b blocks one after another, so the GPU wins from a block count on
 // that is nearly independent of the block size. The crossovers below are measured on the box
 // (bench.py `single_block` and `napi_end_to_end.crossover`; 4 MiB tiles216: compress GPU
-// ~29 ms for one block vs host 1.1 ms per block -> 32 blocks). Decode of up to 160 blocks takes
+// ~29 ms for one block vs host 1.1 ms per block -> 32 blocks). Decode of up to 192 blocks takes
 // the small-batch path (a wave per ~8 KiB of compressed block, round 5): through N-API with a
 // collection before each call, GPU vs host ms 1 block 0.51 vs 0.26, 4: 1.18 vs 1.05, 8: 2.13 vs
 // 2.2-2.4 (profiles/r05_hostio/ab_gc.log), a crossover at ~8 blocks; 8 also keeps frames of a few blocks whose reference-mode decode needs the

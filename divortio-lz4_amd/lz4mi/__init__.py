@@ -35,7 +35,7 @@ GEN_RANDOM, GEN_REPETITIVE, GEN_TILES216 = 0, 1, 2
 GENERATORS = {"random": GEN_RANDOM, "repetitive": GEN_REPETITIVE, "tiles216": GEN_TILES216}
 # decode batches of at most this many blocks take the small-batch path (the library's default,
 # csrc/lz4mi_capi.cpp small_blocks(); LZ4MI_SMALL_BLOCKS changes it, read once per process)
-SMALL_BLOCKS = int(os.environ.get("LZ4MI_SMALL_BLOCKS", "160"))
+SMALL_BLOCKS = int(os.environ.get("LZ4MI_SMALL_BLOCKS", "192"))
 
 # every symbol include/lz4mi.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = ("lz4mi_status_message", "lz4mi_init", "lz4mi_device_count", "lz4mi_version",

@@ -1,4 +1,4 @@
-"""Randomized stress of the small-batch decode path (tool): batches of 1..160 blocks from every
+"""Randomized stress of the small-batch decode path (tool): batches of 1..192 blocks from every
 generator, sizes up to 4 MiB, 0..3 corrupted bytes per block, statuses and bytes against the
 oracle's decode; `--seconds` of batches per run. LZ4MI_SMALL_REPARSE (0/1/2) in the environment
 selects the re-parse test mode."""
@@ -13,7 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--seconds", type=float, default=60)
 ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--min-blocks", type=int, default=1)
-ap.add_argument("--max-blocks", type=int, default=160, help="above 160 (LZ4MI_SMALL_BLOCKS): the batch kernel")
+ap.add_argument("--max-blocks", type=int, default=192, help="above 192 (LZ4MI_SMALL_BLOCKS): the batch kernel")
 ap.add_argument("--js-exact", action="store_true", help="reference mode (LZ4MI_JS_EXACT)")
 ap.add_argument("--random-streams", action="store_true", help="pool of random valid streams (every field shape)")
 ap.add_argument("--dump", default="", help="directory: the first mismatching block's input and outputs (.npz), then stop")
