@@ -235,9 +235,43 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_expand_kernel(ExpArgs a) {
             else hi = mid;
         }
         uint32_t k = lo;
+        uint32_t v[kXBytes];
+        if (x0 + kXBytes <= send && x0 + kXBytes <= n) {
+            // the 16 bytes lie in this segment: they span at most 5 sequences (every sequence but
+            // the block's last writes >= 4 bytes), loaded together -- one round trip, not one per
+            // sequence boundary the lane crosses (text and copy -3..8 %, round 6)
+            // (five named entries, not an array: a select over an array became scratch memory)
+            const uint4 sent = make_uint4(send - base, 0u, 0u, 0u);
+            const uint4 q0 = E[k];
+            const uint4 q1 = k + 1 < cnt ? E[k + 1] : sent;
+            const uint4 q2 = k + 2 < cnt ? E[k + 2] : sent;
+            const uint4 q3 = k + 3 < cnt ? E[k + 3] : sent;
+            const uint4 q4 = k + 4 < cnt ? E[k + 4] : sent;
+#pragma unroll
+            for (int t = 0; t < kXBytes; ++t) {
+                const uint32_t x = x0 + t - base;    // segment-relative
+                uint4 e = q0;
+                if (x >= q1.x) e = q1;
+                if (x >= q2.x) e = q2;
+                if (x >= q3.x) e = q3;
+                if (x >= q4.x) e = q4;
+                if (x - e.x < e.z) {
+                    v[t] = kLit | (e.y + (x - e.x));
+                } else {
+                    const uint32_t ms = base + e.x + e.z, xa = x + base, d = xa - ms;
+                    const int32_t y = (int32_t)(d < e.w ? xa : ms + d % e.w) - (int32_t)e.w;
+                    v[t] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
+                    unres |= y >= 0;
+                }
+            }
+            uint4* P = (uint4*)(a.ptr + (size_t)b * a.x_out_max + x0);
+#pragma unroll
+            for (int q4 = 0; q4 < kXBytes / 4; ++q4) P[q4] = make_uint4(v[4 * q4], v[4 * q4 + 1], v[4 * q4 + 2], v[4 * q4 + 3]);
+            continue;
+        }
+        // (else: the 16 bytes reach past the segment or the output: one sequence at a time)
         uint4 e = E[k];
         uint32_t nxt = k + 1 < cnt ? base + E[k + 1].x : send;
-        uint32_t v[kXBytes];
 #pragma unroll
         for (int t = 0; t < kXBytes; ++t) {
             const uint32_t x = x0 + t;
@@ -398,6 +432,17 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
     for (int q = 0; q < kXBytes / 4; ++q) w[q] = ((const uint4*)P)[q];
     const uint32_t* v = (const uint32_t*)w;
     uint32_t o[kXBytes / 4] = {0, 0, 0, 0};
+    // 16 bytes that are one run of consecutive literal bytes (tiles216: runs of ~50 B): one
+    // unaligned 16-byte load instead of 16 byte loads (tiles216 192 blocks -11 %, round 6)
+    bool run = x0 + kXBytes <= n && (v[0] & kHist) == kLit;
+#pragma unroll
+    for (int t = 1; t < kXBytes; ++t) run = run && v[t] == v[0] + (uint32_t)t;
+    if (run) {
+        uint4 r;
+        __builtin_memcpy(&r, src + (v[0] & 0x3FFFFFFFu), 16);
+        *(uint4*)(dst + x0) = r;
+        continue;
+    }
 #pragma unroll
     for (int t = 0; t < kXBytes; ++t) {
         uint32_t c = 0;
