@@ -32,6 +32,7 @@ struct DecArgs {
     uint32_t xseq_stride = 0;          // entries per block (seg_geom: its segments at s * stride)
     uint32_t xsegs = 0;
     uint32_t x_in_max = 0, x_out_max = 0;
+    int x_flat1 = 0;                   // nearly incompressible blocks (compressed >= 15/16 of the output) take one wave too
     int xphase = 0;                    // 0: speculative parse; 2: re-parse of the disagreeing ones; 1: in order from the first bad entry
     const uint32_t* xfirst = nullptr;  // phase 1: per block, the first segment whose entry was wrong
     uint32_t* xfirst_w = nullptr;      // (written by lz4mi_xverify_kernel)

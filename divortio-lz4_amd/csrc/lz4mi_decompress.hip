@@ -1184,7 +1184,8 @@ __device__ __forceinline__ void decompress_block(const DecArgs& a) {
     // match -- decodes faster in one wave, as in the batch kernel: 1.1 ms for 4 MiB at any batch
     // size, against 0.77 ms alone / 1.57 ms for 16 through the pointers, profiles/r06c)
     const bool xp = XP && (uint32_t)c.in_len <= a.x_in_max && out_cap <= a.x_out_max &&
-                    (uint64_t)out_cap < (uint64_t)c.in_len * kXRatioMax;
+                    (uint64_t)out_cap < (uint64_t)c.in_len * kXRatioMax &&
+                    !(a.x_flat1 && (uint64_t)c.in_len * 16 >= (uint64_t)out_cap * 15);
     // past the export limits (or ratio >= 32): one wave decodes the block as usual -- segment
     // b mod 256, i.e. workgroup 257 b (mod 256 CUs: a CU of its own for every block, where
     // segment 0 would put the blocks of a batch on one CU)
@@ -2183,6 +2184,11 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     a.xfirst = xfirst;
     a.xfirst_w = xfirst;
     a.xforce = force_reparse;
+    // from 64 blocks on, nearly incompressible blocks (compressed >= 15/16 of the output: random data) go to one
+    // wave each too: 4 MiB of literal pointers cost more than a wave's copy once there are many such blocks
+    // (random 64 / 192 blocks 1.76 / 4.79 -> 0.92 / 1.19 ms, the 50/50 mix 192 blocks 6.16 -> 4.83; below 64 a
+    // mix loses: the paced one-wave copies become the critical path -- 32 blocks 1.43 -> 1.62; round 6, profiles/r06fl)
+    a.x_flat1 = nblocks >= 64 ? 1 : 0;
     // phase 0: every segment speculatively; the check; phase 1: the segments from the first
     // wrong entry on (an empty launch when there is none). A phase-1 wave waits only for its
     // predecessor, whose workgroup index is lower (dispatched first): the wait always ends.
