@@ -355,7 +355,7 @@ def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 64, 128, 192, 
     resident: the time is one block's chain latency under the CU's contention). Compress is one
     wave per block at every size."""
     s = stream_obj.cuda_stream
-    res = {"blocks": [], "decompress_ms": [], "compress_ms": []}
+    res = {"blocks": [], "decompress_ms": [], "decompress_reference_ms": [], "compress_ms": []}
 
     def med(fn):
         fn()
@@ -378,6 +378,10 @@ def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 64, 128, 192, 
         res["decompress_ms"].append(med(lambda: lz4mi.decompress_blocks_dev(
             batch.comp.data_ptr(), batch.comp_off.data_ptr(), batch.comp_len.data_ptr(), batch.dec.data_ptr(),
             batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), batch.dec_len.data_ptr(), batch.status.data_ptr(), b, s)))
+        res["decompress_reference_ms"].append(med(lambda: lz4mi.decompress_blocks_dev(   # (the JS layer's default)
+            batch.comp.data_ptr(), batch.comp_off.data_ptr(), batch.comp_len.data_ptr(), batch.dec.data_ptr(),
+            batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), batch.dec_len.data_ptr(), batch.status.data_ptr(), b, s,
+            js_exact=True)))
         res["compress_ms"].append(med(lambda: lz4mi.compress_blocks_dev(
             batch.raw.data_ptr(), batch.raw_off.data_ptr(), batch.raw_len.data_ptr(), scratch.data_ptr(),
             batch.comp_off.data_ptr(), slen.data_ptr(), b, s)))
@@ -386,7 +390,8 @@ def latency_curve(torch, lz4mi, batch, stream_obj, counts=(1, 16, 64, 128, 192, 
     thr = lz4mi.SMALL_BLOCKS   # (the library's default, lz4mi_capi.cpp, or LZ4MI_SMALL_BLOCKS)
     res["decompress_path"] = ["small-batch" if b <= thr else "batch kernel" for b in res["blocks"]]
     res["note"] = (f"device-resident, HIP events; the first b blocks of the headline batch; decode of <= {thr} "
-                   "blocks: small-batch path (LZ4MI_SMALL_BLOCKS), else the batch kernel")
+                   "blocks: small-batch path (LZ4MI_SMALL_BLOCKS), else the batch kernel; decompress_reference_ms: "
+                   "LZ4MI_JS_EXACT, the reference decoder's bytes (the JS layer's default)")
     return res
 
 

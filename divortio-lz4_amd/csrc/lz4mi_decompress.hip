@@ -2209,9 +2209,9 @@ extern "C" hipError_t lz4mi_launch_decompress_small(const uint8_t* in, const uin
     e = lz4mi_launch_expand(in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, xseq, xcnt, xrec,
                             kSegMax, stride, ptr, x_out_max, aux, f1, &redo, nblocks, stream);
     if (e != hipSuccess || !f1) return e;
-    // reference mode (LZ4MI_JS_EXACT): the blocks whose output a double-copy-tail rewrite would
-    // change (lz4mi_xf1_kernel) are decoded again by the batch kernel's in-chunk fix-up; the
-    // launch is empty when there are none
+    // reference mode (LZ4MI_JS_EXACT): the double-copy-tail rewrites were applied to the pointers
+    // (lz4mi_xf1ptr_kernel); a block with a rewrite reading before the block is decoded again by the
+    // batch kernel (LZ4MI_ERR_CROSS_BLOCK when batched); the launch is empty when there is none
     lz4mi::DecArgs r{in, in_off, in_len, out, out_off, out_cap, dict, dict_len, out_len, status, nblocks,
                      nblocks > 1 ? 1 : 0, 1};
     r.redo = redo;

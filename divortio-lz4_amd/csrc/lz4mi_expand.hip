@@ -384,12 +384,17 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
   }
 }
 
-// Reference mode (LZ4MI_JS_EXACT): would the reference's double-copy-tail rewrite
-// (blockDecompress.js:219-250, SURVEY.md F1: offset >= 8, length < 8) change a byte of the
-// finished output? The spec output is the reference's exactly when no rewrite changes a byte (a
-// rewrite reads bytes before its match, final by then, that no later rewrite touches); a block
-// with one is decoded again by the batch kernel's fix-up (redo[b]). One workgroup per segment.
-__global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int isolate, uint32_t* redo) {
+// Reference mode (LZ4MI_JS_EXACT) in pointer form (round 6; until then a check after the gather sent every
+// block whose output a rewrite would change to the batch kernel's fix-up: one wave, ~8 ms for 4 MiB): the
+// reference's tail rewrite for a match at s (offset >= 8, length < 8, blockDecompress.js:219-250) sets
+// out[p] = out[p - off] for p in [s + ml - 8, s) after the match is copied. Here those bytes' pointers become
+// p - off before the rounds, which is exact: off >= 8 puts p - off below the region, where it is final (a
+// later rewrite starts at or after its own match start - 4 >= s, matches write a byte once); no later rewrite
+// reaches the region; a read of a region byte before the rewrite can only come from a later byte of the same
+// region (the region spans <= 4 bytes before s), which the rewrite overwrites too; and every read after it
+// goes through the new pointer. A rewrite reading before the block still goes to the batch kernel (redo[b]:
+// LZ4MI_ERR_CROSS_BLOCK when batched). One workgroup per segment.
+__global__ __launch_bounds__(kXThreads) void lz4mi_xf1ptr_kernel(ExpArgs a, uint32_t* redo) {
     const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return;
     const SegGeom G = seg_geom(a.in_len[b]);
@@ -398,9 +403,9 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int iso
     const uint32_t base = R[sg].base, send = base + R[sg].olen, cnt = R[sg].cnt;
     const uint4* E = seg_entries(a, b, sg, G);
     const int64_t out_off = (int64_t)a.out_off[b];
-    const int64_t cap = min(a.out_len[b], a.out_cap[b]);
-    const uint8_t* dst = a.out + out_off;
-    bool ch = false;
+    const int64_t n = min(a.out_len[b], a.out_cap[b]);
+    uint32_t* P = a.ptr + (size_t)b * a.x_out_max;
+    bool any = false, cross = false;
     for (uint32_t k = threadIdx.x; k < cnt; k += kXThreads) {
         const uint4 e = E[k];
         const int64_t ms = (int64_t)base + e.x + e.z, off = e.w;
@@ -408,13 +413,16 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_xf1_kernel(ExpArgs a, int iso
         if (ml == 0 || ml >= 8 || off < 8 || out_off + ms - off < 0) continue;
         const int64_t p0 = ms + ml - 8;
         if (p0 - off < 0) {
-            ch = true;   // (batched: reported as LZ4MI_ERR_CROSS_BLOCK by the redo)
+            cross = true;   // (batched: reported as LZ4MI_ERR_CROSS_BLOCK by the redo)
             continue;
         }
-        for (int64_t q = p0; q < ms && q < cap; ++q) ch |= dst[q] != dst[q - off];
+        for (int64_t q = p0; q < ms && q < n; ++q) {
+            P[q] = (uint32_t)(q - off);
+            any = true;
+        }
     }
-    (void)isolate;
-    if (ch) redo[b] = 1u;
+    if (cross) redo[b] = 1u;
+    if (__syncthreads_or(any) && threadIdx.x == 0) a.flags[0] = 1u;
 }
 
 __global__ __launch_bounds__(kXThreads) void lz4mi_gather_kernel(ExpArgs a) {
@@ -494,11 +502,9 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
     hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     const dim3 grid(min(a.ntiles, kXGrid));
     hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
+    if (f1) hipLaunchKernelGGL(lz4mi_xf1ptr_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, redo);
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
     hipLaunchKernelGGL(lz4mi_chase_kernel, grid, dim3(kXThreads), 0, stream, a);
     hipLaunchKernelGGL(lz4mi_gather_kernel, grid, dim3(kXThreads), 0, stream, a);
-    if (f1)
-        hipLaunchKernelGGL(lz4mi_xf1_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0,
-                           redo);
     return hipGetLastError();
 }
