@@ -392,9 +392,10 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_chase_kernel(ExpArgs a) {
 // later rewrite starts at or after its own match start - 4 >= s, matches write a byte once); no later rewrite
 // reaches the region; a read of a region byte before the rewrite can only come from a later byte of the same
 // region (the region spans <= 4 bytes before s), which the rewrite overwrites too; and every read after it
-// goes through the new pointer. A rewrite reading before the block still goes to the batch kernel (redo[b]:
-// LZ4MI_ERR_CROSS_BLOCK when batched). One workgroup per segment.
-__global__ __launch_bounds__(kXThreads) void lz4mi_xf1ptr_kernel(ExpArgs a, uint32_t* redo) {
+// goes through the new pointer. A rewrite reading before the block points into the caller's array (0 before
+// it, as the reference reads a missing index); batched, writing before the block, or reading before the
+// array with a dictionary, the block goes to the batch kernel (redo[b]: LZ4MI_ERR_CROSS_BLOCK when batched). One workgroup per segment.
+__global__ __launch_bounds__(kXThreads) void lz4mi_xf1ptr_kernel(ExpArgs a, int isolate, uint32_t* redo) {
     const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (a.status[b] != 0 || a.xcnt[b] == kNotExported) return;
     const SegGeom G = seg_geom(a.in_len[b]);
@@ -412,12 +413,18 @@ __global__ __launch_bounds__(kXThreads) void lz4mi_xf1ptr_kernel(ExpArgs a, uint
         const int64_t ml = (k + 1 < cnt ? (int64_t)base + E[k + 1].x : (int64_t)send) - ms;
         if (ml == 0 || ml >= 8 || off < 8 || out_off + ms - off < 0) continue;
         const int64_t p0 = ms + ml - 8;
-        if (p0 - off < 0) {
-            cross = true;   // (batched: reported as LZ4MI_ERR_CROSS_BLOCK by the redo)
+        if (p0 - off < 0 && (isolate || (p0 < 0 && out_off > 0) || (a.dict && out_off + p0 - off < 0))) {
+            // batched: reported as LZ4MI_ERR_CROSS_BLOCK by the redo; a region starting before the block
+            // rewrites the caller's bytes before it (the reference's indices are absolute); with a
+            // dictionary, a read before the array is the reference's 0, not a dictionary byte
+            cross = true;
             continue;
         }
-        for (int64_t q = p0; q < ms && q < n; ++q) {
-            P[q] = (uint32_t)(q - off);
+        for (int64_t q = p0 > 0 ? p0 : 0; q < ms && q < n; ++q) {
+            // before the block: the caller's bytes in the array, or 0 before the array (the reference's read
+            // of a missing index): a history pointer, gathered the same way
+            const int64_t y = q - off;
+            P[q] = y >= 0 ? (uint32_t)y : (kHist | (uint32_t)(y + 65536));
             any = true;
         }
     }
@@ -502,7 +509,9 @@ extern "C" hipError_t lz4mi_launch_expand(const uint8_t* in, const uint64_t* in_
     hipLaunchKernelGGL(lz4mi_xstatus_kernel, dim3(nblocks), dim3(64), 0, stream, a);
     const dim3 grid(min(a.ntiles, kXGrid));
     hipLaunchKernelGGL(lz4mi_expand_kernel, grid, dim3(kXThreads), 0, stream, a);
-    if (f1) hipLaunchKernelGGL(lz4mi_xf1ptr_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, redo);
+    if (f1)
+        hipLaunchKernelGGL(lz4mi_xf1ptr_kernel, dim3(nseg, nblocks), dim3(kXThreads), 0, stream, a, nblocks > 1 ? 1 : 0,
+                           redo);
     for (int r = 0; r < kJumpRounds; ++r) hipLaunchKernelGGL(lz4mi_jump_kernel, grid, dim3(kXThreads), 0, stream, a, r);
     hipLaunchKernelGGL(lz4mi_chase_kernel, grid, dim3(kXThreads), 0, stream, a);
     hipLaunchKernelGGL(lz4mi_gather_kernel, grid, dim3(kXThreads), 0, stream, a);
